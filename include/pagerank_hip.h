@@ -1,0 +1,158 @@
+/*
+ * libpagerank_hip -- C ABI of the MI355X (gfx950) PageRank engine that replaces the power
+ * iteration of Sparky.java (mayursharma/PageRank-using-Apache-Spark).
+ *
+ * The reference has no plugin/FFI interface: its hot path is inline Spark transformations in
+ * main() (Sparky.java:124-238).  This header is the drop-in boundary a JVM host binds through
+ * Panama FFM or JNI.  Each entry point names the reference code it
+ * replaces.  Plain pointers and sizes only; every function returns PR_OK (0) or a negative
+ * PR_ERR_* code with a thread-local message in pr_last_error(); nothing throws across the ABI.
+ *
+ * Ownership: pointer inputs are caller-owned and borrowed only for the duration of the call.
+ * Device memory is owned by the library and released by pr_graph_destroy().  Outputs are
+ * caller-allocated.  A pr_graph handle is not re-entrant; distinct handles may be used from
+ * distinct threads.
+ *
+ * Vertex IDs are dense int32 IDs produced by the host's URL interner (first appearance,
+ * src before dst).  Every ID in [0, n_vertices) must appear in the edge list.  dst[i] == -1
+ * marks a record without any type=="a" link (Sparky.java:114-118: "(url, null)").
+ */
+#ifndef PAGERANK_HIP_H
+#define PAGERANK_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PR_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define PR_OK 0
+#define PR_ERR_INVALID (-1)  /* bad argument / malformed edge list                        */
+#define PR_ERR_HIP (-2)      /* HIP runtime failure                                        */
+#define PR_ERR_OOM (-3)      /* device or host allocation failed                           */
+#define PR_ERR_COMM (-4)     /* RCCL failure                                               */
+#define PR_ERR_STATE (-5)    /* call not valid in the handle's current state               */
+#define PR_ERR_NODEVICE (-6) /* no usable GPU                                              */
+
+/* ---- graph creation flags ------------------------------------------------------------ */
+#define PR_DANGLING_LOCAL 0u /* Spark local[N] semantics: D = sink-only vertices (default) */
+#define PR_DANGLING_NONE 1u  /* cluster-mode semantics: dangUrls empty on the driver, dc=0 */
+#define PR_INPUT_DEVICE 2u   /* src/dst are device pointers on `device` (not host)        */
+#define PR_NO_CANONICAL 4u   /* drop the canonical CSR after the build (no export)        */
+
+/* ---- vertex flag bits (pr_graph_export_csr vflags) ---------------------------------- */
+#define PR_VF_KEY 1u    /* vertex is a record key / src          Sparky.java:127-135      */
+#define PR_VF_SINK 2u   /* target never seen as a record         Sparky.java:146-149      */
+#define PR_VF_NOLINK 4u /* record whose only value is null       Sparky.java:114-118      */
+#define PR_VF_INDEG0 8u /* no in-link: keeps its old rank as sum Sparky.java:224-225      */
+
+/* ---- pr_graph_info indices ------------------------------------------------------------ */
+#define PR_INFO_N_VERTICES 0   /* N = totalUrlCount (Sparky.java:162)                       */
+#define PR_INFO_N_EDGES 1      /* E' = distinct edges (Sparky.java:124)                      */
+#define PR_INFO_N_SINK 2       /* |D| in local mode (Sparky.java:172-184)                    */
+#define PR_INFO_N_NOLINK 3     /* keys without links (their mass leaks)                     */
+#define PR_INFO_N_INDEG0 4     /* vertices hit by the subtractByKey quirk                   */
+#define PR_INFO_MAX_INDEG 5
+#define PR_INFO_LOCAL_ROWS 6   /* rows owned by this part                                   */
+#define PR_INFO_LOCAL_EDGES 7  /* in-links owned by this part                               */
+#define PR_INFO_PART 8
+#define PR_INFO_N_PARTS 9
+#define PR_INFO_N_UNITS 10     /* work units of the SpMV launch                             */
+#define PR_INFO_N_LONG_ROWS 11 /* rows split across several units                          */
+#define PR_INFO_DEVICE_BYTES 12
+#define PR_INFO_COUNT 13
+
+/* ---- pr_get_stats indices ------------------------------------------------------------- */
+#define PR_STAT_ITERS 0          /* iterations run since the last reset                     */
+#define PR_STAT_LAST_DC 1        /* danglingContrib used by the last iteration              */
+#define PR_STAT_LAST_L1 2        /* sum |r_k - r_{k-1}| of the last iteration                */
+#define PR_STAT_SPMV_MS_MEAN 3   /* mean HIP-event time of the SpMV launch (timing on)      */
+#define PR_STAT_SPMV_LAUNCHES 4  /* SpMV launches timed                                     */
+#define PR_STAT_ITER_MS_MEAN 5   /* mean HIP-event time of a whole iteration (timing on)    */
+#define PR_STAT_BUILD_MS 6       /* wall time of the graph build                            */
+#define PR_STAT_EXCHANGE_MS_MEAN 7 /* mean time of the RCCL exchange (parts > 1)            */
+#define PR_STAT_COUNT 8
+
+typedef struct pr_graph pr_graph;
+
+/* Per-iteration callback (runs on the calling thread between iterations).
+ * ranks_or_null: V doubles in original-ID order when PR_CB_RANKS is set (else NULL);
+ * for a part, only the part's own vertices are written, the rest hold the previous content. */
+typedef void (*pr_iter_cb)(int32_t iter, const double *ranks_or_null, double dangling_sum,
+                           double l1_delta, double ms, void *user);
+#define PR_CB_RANKS 1u
+
+int pr_abi_version(void);
+const char *pr_last_error(void);
+int pr_device_count(int32_t *out);
+
+/* Graph construction: replaces Sparky.java:124-184 (distinct/groupByKey, key broadcast,
+ * sink completion, union/count, dangling fixup).  Builds the canonical in-link CSR on the
+ * GPU (radix sort + dedupe) and the internal degree-ordered layout used by the iteration.
+ * src/dst: n_edges raw interned edges (duplicates and self-loops allowed, dst = -1 for a
+ * record without links).  Host pointers unless PR_INPUT_DEVICE. */
+int pr_graph_create(int32_t device, int32_t n_vertices, int64_t n_edges, const int32_t *src,
+                    const int32_t *dst, uint32_t flags, pr_graph **out);
+
+/* The same, keeping only the rows of `part` out of `n_parts` (1D row partition for one
+ * process per GPU).  Every part must be created from the same edge list. */
+int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices,
+                         int64_t n_edges, const int32_t *src, const int32_t *dst, uint32_t flags,
+                         pr_graph **out);
+
+/* info[i] for i < min(n_info, PR_INFO_COUNT). */
+int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info);
+
+/* Canonical CSR (rows = dst, columns = src ascending, deduplicated) in original IDs, for
+ * bit-exact tests.  row_ptr[V+1], col_idx[E'], out_deg[V], vflags[V]; any may be NULL. */
+int pr_graph_export_csr(const pr_graph *g, int64_t *row_ptr, int32_t *col_idx, int32_t *out_deg,
+                        uint8_t *vflags);
+
+/* Whole job: replaces Sparky.java:164-238.  Resets ranks to init_ranks (NULL = 1.0 for every
+ * vertex, Sparky.java:165-170), runs `iterations` steps of
+ * r' = teleport + damping * (S + dc / N) and copies the final ranks (original-ID order, V
+ * doubles) to ranks_out (may be NULL).  cb (may be NULL) is called after every iteration. */
+int pr_run(pr_graph *g, int32_t iterations, double teleport, double damping,
+           const double *init_ranks, double *ranks_out, pr_iter_cb cb, uint32_t cb_flags,
+           void *user);
+
+/* Lower-level stepping (resume from saved ranks, benchmarking).  pr_step enqueues work on
+ * the library's stream and returns; pr_sync waits for it. */
+int pr_reset(pr_graph *g, double teleport, double damping, const double *init_ranks);
+int pr_step(pr_graph *g, int32_t iterations);
+int pr_sync(pr_graph *g);
+int pr_get_ranks(pr_graph *g, double *ranks_out);
+int pr_set_timing(pr_graph *g, int32_t enable);
+int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
+
+/* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes
+ * to every rank (any channel), every rank attaches it to its part.  Parts exchange the
+ * contribution vector with an RCCL all-gather over xGMI once per iteration. */
+#define PR_COMM_ID_BYTES 128
+int pr_comm_unique_id(uint8_t *id_out);
+int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8_t *id);
+
+void pr_graph_destroy(pr_graph *g);
+
+/* ---- synthetic inputs and device-side interning (benchmark front-end) ----------------- */
+/* R-MAT (Graph500 parameters a,b,c, d = 1-a-b-c), n_edges edges over 2^scale labels, labels
+ * scrambled by a seeded bijection.  d_src/d_dst: device arrays of n_edges int32. */
+int pr_gen_rmat(int32_t device, int32_t scale, int64_t n_edges, double a, double b, double c,
+                uint64_t seed, int32_t *d_src, int32_t *d_dst);
+/* Uniform Erdos-Renyi G(n, m): src, dst uniform over 2^scale labels. */
+int pr_gen_er(int32_t device, int32_t scale, int64_t n_edges, uint64_t seed, int32_t *d_src,
+              int32_t *d_dst);
+/* Relabel raw labels in [0, label_bound) to dense IDs in first-appearance order (src before
+ * dst, edge by edge) -- the same mapping the host URL interner produces -- in place.
+ * dst == -1 entries are kept.  *n_vertices_out = number of distinct labels. */
+int pr_intern_device(int32_t device, int64_t n_edges, int32_t label_bound, int32_t *d_src,
+                     int32_t *d_dst, int32_t *n_vertices_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PAGERANK_HIP_H */

@@ -1,0 +1,169 @@
+"""Oracle #1 -- literal RDD-level restatement of Sparky.java's PageRank (TEST INFRASTRUCTURE).
+
+This module is a *checker*, not product code.  Only ``tests/``, ``__graft_entry__.smoke()``
+and ``bench.py``'s ``cpu_baseline`` leg may import it.  The product path
+(``libpagerank_hip``) never routes through it.
+
+It emulates, on Python dicts/sets, the Spark operators Sparky.java applies, line by line,
+so that every quirk of the reference survives:
+
+* ``pairs`` is the output of the link-extraction ``flatMapToPair`` (Sparky.java:78-123):
+  ``(url, href)`` for each ``type=="a"`` link (:107) and ``(url, None)`` for a record with
+  no ``a`` link (:114-118, which also does ``dangUrls.add(url)``).  The edge-list
+  front-end maps a line ``u v`` to ``(u, v)`` and a single-token line ``u`` to ``(u, None)``.
+* ``distinct().groupByKey()`` (:124), key collect/broadcast (:127-135), sink completion
+  (:137-159), ``union`` (:161), ``count`` (:162), rank init to 1.0 (:165-170), the
+  dangling-set fixup with ``lookup`` (:172-184), and the 10-iteration loop (:187-238):
+  join/flatMap contributions (:192-216), dangling sum (:219-222), ``subtractByKey`` +
+  ``union`` in-degree-0 quirk (:224-225), ``reduceByKey(Sum)`` + affine update (:229-235).
+
+Parity status: **unpinned against a run of the reference** -- the reference cannot run here
+(no JDK/Spark in the image) and ships no tests or golden vectors.  The
+emulator is pinned to the hand-derived known-answer test of SURVEY.md §4 (see
+``tests/test_oracle.py``) and cross-checked against the C restatement ``pagerank_oracle.c``.
+
+Summation order: Spark's ``reduceByKey`` and the driver's HashSet iteration order are
+unspecified (Sparky.java:219-222, :229); this oracle uses exactly rounded sums
+(``math.fsum``), the order-independent ideal that any Spark order approximates to ~1 ulp·n.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Dict, Hashable, Iterable, List, Optional, Sequence, Tuple
+
+TELEPORT = 0.15  # Sparky.java:233
+DAMPING = 0.85  # Sparky.java:233
+
+
+def pairs_from_edge_lines(lines: Iterable[str]) -> List[Tuple[str, Optional[str]]]:
+    """Edge-list front-end: ``u v`` -> (u, v); ``u`` -> (u, None) (Sparky.java:107, :116).
+
+    Tokens are taken verbatim (whitespace separated).  Blank lines are ignored.  Extra
+    tokens beyond the second are an error (the product reader rejects them too).
+    """
+    out: List[Tuple[str, Optional[str]]] = []
+    for ln, line in enumerate(lines):
+        toks = line.split()
+        if not toks:
+            continue
+        if len(toks) == 1:
+            out.append((toks[0], None))
+        elif len(toks) == 2:
+            out.append((toks[0], toks[1]))
+        else:
+            raise ValueError(f"line {ln + 1}: expected 1 or 2 tokens, got {len(toks)}")
+    return out
+
+
+def intern_first_appearance(pairs: Sequence[Tuple[str, Optional[str]]]):
+    """Canonical ID mapping: first appearance, ``src`` before ``dst``.
+
+    Returns ``(names, src_ids, dst_ids)`` with ``dst_ids[i] == -1`` for a no-link record.
+    """
+    ids: Dict[str, int] = {}
+    names: List[str] = []
+    src_ids: List[int] = []
+    dst_ids: List[int] = []
+    for u, v in pairs:
+        if u not in ids:
+            ids[u] = len(names)
+            names.append(u)
+        src_ids.append(ids[u])
+        if v is None:
+            dst_ids.append(-1)
+        else:
+            if v not in ids:
+                ids[v] = len(names)
+                names.append(v)
+            dst_ids.append(ids[v])
+    return names, src_ids, dst_ids
+
+
+class SparkyRDD:
+    """Graph construction of Sparky.java:124-184, kept as dict-shaped 'RDDs'."""
+
+    def __init__(self, pairs: Sequence[Tuple[Hashable, Optional[Hashable]]], dangling: str = "local"):
+        if dangling not in ("local", "none"):
+            raise ValueError("dangling must be 'local' or 'none'")
+        self.dangling = dangling
+        # Sparky.java:117 -- dangUrls.add(url) for records without 'a' links.  In cluster mode
+        # the executor-side static never reaches the driver: D stays empty.
+        dang_urls = set()
+        if dangling == "local":
+            dang_urls.update(u for u, t in pairs if t is None)
+        # Sparky.java:124 -- .distinct().groupByKey(); insertion order is irrelevant.
+        links: "OrderedDict[Hashable, List[Optional[Hashable]]]" = OrderedDict()
+        for u, t in OrderedDict.fromkeys(pairs):
+            links.setdefault(u, []).append(t)
+        # Sparky.java:127-135 -- key set broadcast.
+        key_set = set(links)
+        # Sparky.java:137-159 -- sink completion: (url, null) for every target not a key.
+        sinks: "OrderedDict[Hashable, None]" = OrderedDict()
+        for _k, lst in links.items():
+            # arg._2 is never null after groupByKey, so the else-branch (:152-155) is dead.
+            for url in lst:
+                if url not in key_set and url is not None:
+                    if dangling == "local":
+                        dang_urls.add(url)  # :148
+                    sinks[url] = None
+        # Sparky.java:161 -- union; keys are disjoint by construction.
+        self.all_urls: "OrderedDict[Hashable, Optional[List[Optional[Hashable]]]]" = OrderedDict(links)
+        for s in sinks:
+            self.all_urls[s] = None
+        # Sparky.java:162 -- totalUrlCount.
+        self.total_url_count = len(self.all_urls)
+        # Sparky.java:172-184 -- fixup: keep s only if lookup(s) is [null].
+        not_dangling = set()
+        for s in dang_urls:
+            look = [self.all_urls[s]] if s in self.all_urls else []
+            if not (look is None or len(look) == 0 or (len(look) == 1 and look[0] is None)):
+                not_dangling.add(s)
+        self.dang_urls = dang_urls - not_dangling
+
+    def initial_ranks(self) -> Dict[Hashable, float]:
+        """Sparky.java:165-170 -- every URL starts at rank 1.0 (no 1/N normalisation)."""
+        return {u: 1.0 for u in self.all_urls}
+
+    def iterate(self, ranks: Dict[Hashable, float]) -> Tuple[Dict[Hashable, float], float]:
+        """One pass of Sparky.java:189-235. Returns (new_ranks, danglingContrib)."""
+        # :192-216 -- contributions.
+        contribs: Dict[Hashable, List[float]] = {}
+        for u, lst in self.all_urls.items():
+            if lst is None:
+                continue  # sink-only vertex: null Iterable, emits nothing (:198)
+            url_count = len(lst)  # Iterables.size counts nulls (:199)
+            for s in lst:
+                if s is None:
+                    url_count -= 1  # :200-205
+            if url_count == 0:
+                continue  # r/0 = +Inf in Java (:207) but nothing is emitted (:208-211)
+            page_rank = ranks[u] / url_count  # one fp64 division (:207)
+            for s in lst:
+                if s is not None:
+                    contribs.setdefault(s, []).append(page_rank)
+        # :219-222 -- danglingContrib over the fixed-up dangUrls (sink-only vertices).
+        dc = math.fsum(ranks[u] for u in self.dang_urls)
+        # :224-225 -- vertices without a contribution re-use their OLD rank as the "sum".
+        for u in ranks:
+            if u not in contribs:
+                contribs[u] = [ranks[u]]
+        # :229-235 -- reduceByKey(Sum) then 0.15 + 0.85 * (sum + dc / N).
+        n = float(self.total_url_count)
+        new_ranks = {}
+        for u in ranks:
+            s = math.fsum(contribs[u])
+            new_ranks[u] = TELEPORT + DAMPING * (s + dc / n)
+        return new_ranks, dc
+
+
+def run(pairs, iterations: int = 10, dangling: str = "local", init: Optional[Dict] = None):
+    """Run the whole job; returns (graph, list of per-iteration rank dicts, list of dc)."""
+    g = SparkyRDD(pairs, dangling=dangling)
+    ranks = dict(init) if init is not None else g.initial_ranks()
+    history, dcs = [], []
+    for _ in range(iterations):  # Sparky.java:187
+        ranks, dc = g.iterate(ranks)
+        history.append(ranks)
+        dcs.append(dc)
+    return g, history, dcs

@@ -1,0 +1,334 @@
+// C ABI of libpagerank_hip (include/pagerank_hip.h): handle management, error reporting,
+// the run loop with its per-iteration callback, export, and the RCCL exchange.
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "pr_graph.h"
+
+namespace pr {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int DevBuf::alloc(size_t n) {
+  reset();
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc(&p, n);
+  if (e != hipSuccess) {
+    p = nullptr;
+    (void)hipGetLastError();
+    return fail(PR_ERR_OOM, "hipMalloc(" + std::to_string(n) + " bytes) failed: " + hipGetErrorString(e));
+  }
+  bytes = n;
+  return PR_OK;
+}
+
+void DevBuf::reset() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+// All-gather of the contribution slices (+ the two slots) across parts: the only data
+// exchange of the row-partitioned iteration.  In place: part p's slice is
+// already at offset p * S_pad of the buffer.
+int exchange(pr_graph *g, int buf) {
+  if (g->nparts <= 1) return PR_OK;
+  if (!g->comm) return fail(PR_ERR_STATE, "graph part has no communicator (pr_graph_attach_comm)");
+  double *base = g->cbuf[buf].as<double>();
+  ncclResult_t rc = ncclAllGather(base + (int64_t)g->part * g->S_pad, base, (size_t)g->S_pad,
+                                  ncclDouble, g->comm, g->stream);
+  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+  return PR_OK;
+}
+
+}  // namespace pr
+
+size_t pr_graph::device_bytes() const {
+  size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
+  b += rowptr.bytes + col.bytes + degf.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
+  b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
+  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes;
+  return b;
+}
+
+using pr::fail;
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int check_device(int32_t device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return fail(PR_ERR_NODEVICE, "no HIP device available");
+  }
+  if (device < 0 || device >= n) return fail(PR_ERR_INVALID, "device index out of range");
+  return PR_OK;
+}
+
+int create_common(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
+                  const int32_t *src, const int32_t *dst, uint32_t flags, pr_graph **out) {
+  if (!out) return fail(PR_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  if (n_parts < 1 || part < 0 || part >= n_parts) return fail(PR_ERR_INVALID, "bad part / n_parts");
+  if (n_vertices < 0 || n_edges < 0) return fail(PR_ERR_INVALID, "negative size");
+  if (n_edges > 0 && (!src || !dst)) return fail(PR_ERR_INVALID, "src/dst is NULL");
+  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL)) return fail(PR_ERR_INVALID, "unknown flag bits");
+  PR_TRY(check_device(device));
+  DeviceGuard dg(device);
+  pr_graph *g = new (std::nothrow) pr_graph();
+  if (!g) return fail(PR_ERR_OOM, "host allocation failed");
+  g->device = device;
+  g->flags = flags;
+  g->V = n_vertices;
+  g->part = part;
+  g->nparts = n_parts;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete g;
+    return fail(PR_ERR_HIP, "hipStreamCreate failed");
+  }
+  int rc = pr::build_graph(g, n_edges, src, dst);
+  if (rc != PR_OK) {
+    std::string msg = pr_last_error();
+    pr_graph_destroy(g);
+    pr::set_error(msg);
+    return rc;
+  }
+  *out = g;
+  return PR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pr_abi_version(void) { return PR_ABI_VERSION; }
+
+const char *pr_last_error(void) { return pr::g_last_error.c_str(); }
+
+int pr_device_count(int32_t *out) {
+  if (!out) return fail(PR_ERR_INVALID, "out is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  *out = n;
+  return PR_OK;
+}
+
+int pr_graph_create(int32_t device, int32_t n_vertices, int64_t n_edges, const int32_t *src,
+                    const int32_t *dst, uint32_t flags, pr_graph **out) {
+  return create_common(device, 0, 1, n_vertices, n_edges, src, dst, flags, out);
+}
+
+int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices,
+                         int64_t n_edges, const int32_t *src, const int32_t *dst, uint32_t flags,
+                         pr_graph **out) {
+  return create_common(device, part, n_parts, n_vertices, n_edges, src, dst, flags, out);
+}
+
+int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
+  if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
+  const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
+                                    g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
+                                    g->n_units,   g->n_long,   (int64_t)g->device_bytes()};
+  for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
+  return PR_OK;
+}
+
+int pr_graph_export_csr(const pr_graph *g, int64_t *row_ptr, int32_t *col_idx, int32_t *out_deg,
+                        uint8_t *vflags) {
+  if (!g) return fail(PR_ERR_INVALID, "NULL graph");
+  if (!g->has_canonical) return fail(PR_ERR_STATE, "canonical CSR was dropped (PR_NO_CANONICAL)");
+  DeviceGuard dg(g->device);
+  hipStream_t s = g->stream;
+  if (row_ptr)
+    PR_HIP(hipMemcpyAsync(row_ptr, g->canon_rowptr.p, sizeof(int64_t) * ((size_t)g->V + 1), hipMemcpyDeviceToHost, s));
+  if (col_idx && g->E_dedup > 0)
+    PR_HIP(hipMemcpyAsync(col_idx, g->canon_col.p, sizeof(int32_t) * g->E_dedup, hipMemcpyDeviceToHost, s));
+  if (out_deg && g->V > 0)
+    PR_HIP(hipMemcpyAsync(out_deg, g->canon_deg.p, sizeof(int32_t) * g->V, hipMemcpyDeviceToHost, s));
+  if (vflags && g->V > 0)
+    PR_HIP(hipMemcpyAsync(vflags, g->canon_vflags.p, (size_t)g->V, hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  return PR_OK;
+}
+
+int pr_reset(pr_graph *g, double teleport, double damping, const double *init_ranks) {
+  if (!g) return fail(PR_ERR_INVALID, "NULL graph");
+  DeviceGuard dg(g->device);
+  g->teleport = teleport;
+  g->damping = damping;
+  return pr::iter_reset(g, init_ranks);
+}
+
+int pr_step(pr_graph *g, int32_t iterations) {
+  if (!g || iterations < 0) return fail(PR_ERR_INVALID, "bad argument");
+  DeviceGuard dg(g->device);
+  return pr::iter_step(g, iterations);
+}
+
+int pr_sync(pr_graph *g) {
+  if (!g) return fail(PR_ERR_INVALID, "NULL graph");
+  DeviceGuard dg(g->device);
+  PR_HIP(hipStreamSynchronize(g->stream));
+  return PR_OK;
+}
+
+int pr_get_ranks(pr_graph *g, double *ranks_out) {
+  if (!g || !ranks_out) return fail(PR_ERR_INVALID, "NULL argument");
+  if (!g->ready) return fail(PR_ERR_STATE, "pr_get_ranks before pr_reset");
+  DeviceGuard dg(g->device);
+  std::vector<double> loc((size_t)g->n_local);
+  if (g->n_local > 0)
+    PR_HIP(hipMemcpyAsync(loc.data(), g->r.p, sizeof(double) * g->n_local, hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  for (int64_t j = 0; j < g->n_local; ++j) ranks_out[g->orig_of_local[j]] = loc[j];
+  return PR_OK;
+}
+
+int pr_set_timing(pr_graph *g, int32_t enable) {
+  if (!g) return fail(PR_ERR_INVALID, "NULL graph");
+  g->timing = enable != 0;
+  return PR_OK;
+}
+
+int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
+  if (!g || !stats) return fail(PR_ERR_INVALID, "NULL argument");
+  DeviceGuard dg(g->device);
+  PR_HIP(hipStreamSynchronize(g->stream));
+  auto mean_ms = [&](const std::vector<std::pair<int, int>> &ev, double *out) -> int {
+    double acc = 0.0;
+    for (auto &pr_ : ev) {
+      float ms = 0.f;
+      PR_HIP(hipEventElapsedTime(&ms, g->ev_pool[pr_.first], g->ev_pool[pr_.second]));
+      acc += ms;
+    }
+    *out = ev.empty() ? 0.0 : acc / (double)ev.size();
+    return PR_OK;
+  };
+  double v[PR_STAT_COUNT] = {0};
+  v[PR_STAT_ITERS] = (double)g->iters_done;
+  if (g->ready) {
+    PR_TRY(pr::read_slots(g, g->cur, &v[PR_STAT_LAST_DC], &v[PR_STAT_LAST_L1]));
+    // the dc *used* by the last iteration lives in the previous buffer
+    if (g->iters_done > 0) {
+      double dc_prev = 0, l1_prev = 0;
+      PR_TRY(pr::read_slots(g, g->cur ^ 1, &dc_prev, &l1_prev));
+      v[PR_STAT_LAST_DC] = dc_prev;
+    } else {
+      v[PR_STAT_LAST_L1] = 0.0;
+    }
+  }
+  PR_TRY(mean_ms(g->spmv_ev, &v[PR_STAT_SPMV_MS_MEAN]));
+  v[PR_STAT_SPMV_LAUNCHES] = (double)g->spmv_ev.size();
+  PR_TRY(mean_ms(g->iter_ev, &v[PR_STAT_ITER_MS_MEAN]));
+  v[PR_STAT_BUILD_MS] = g->build_ms;
+  PR_TRY(mean_ms(g->xchg_ev, &v[PR_STAT_EXCHANGE_MS_MEAN]));
+  for (int32_t i = 0; i < n_stats && i < PR_STAT_COUNT; ++i) stats[i] = v[i];
+  return PR_OK;
+}
+
+int pr_run(pr_graph *g, int32_t iterations, double teleport, double damping,
+           const double *init_ranks, double *ranks_out, pr_iter_cb cb, uint32_t cb_flags,
+           void *user) {
+  if (!g || iterations < 0) return fail(PR_ERR_INVALID, "bad argument");
+  DeviceGuard dg(g->device);
+  g->teleport = teleport;
+  g->damping = damping;
+  PR_TRY(pr::iter_reset(g, init_ranks));
+  std::vector<double> cb_ranks;
+  if (cb && (cb_flags & PR_CB_RANKS)) {
+    cb_ranks.assign((size_t)g->V, 0.0);
+    if (init_ranks) std::memcpy(cb_ranks.data(), init_ranks, sizeof(double) * g->V);
+  }
+  for (int32_t it = 0; it < iterations; ++it) {
+    if (!cb) {
+      PR_TRY(pr::iter_step(g, iterations));
+      break;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    double dc = 0, l1 = 0, dummy = 0;
+    PR_TRY(pr::read_slots(g, g->cur, &dc, &dummy));  // dc used by this iteration
+    PR_TRY(pr::iter_step(g, 1));
+    PR_HIP(hipStreamSynchronize(g->stream));
+    PR_TRY(pr::read_slots(g, g->cur, &dummy, &l1));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const double *rp = nullptr;
+    if (cb_flags & PR_CB_RANKS) {
+      PR_TRY(pr_get_ranks(g, cb_ranks.data()));
+      rp = cb_ranks.data();
+    }
+    cb(it, rp, dc, l1, ms, user);
+  }
+  PR_HIP(hipStreamSynchronize(g->stream));
+  if (ranks_out) PR_TRY(pr_get_ranks(g, ranks_out));
+  return PR_OK;
+}
+
+int pr_comm_unique_id(uint8_t *id_out) {
+  if (!id_out) return fail(PR_ERR_INVALID, "NULL argument");
+  static_assert(sizeof(ncclUniqueId) == PR_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t rc = ncclGetUniqueId(&id);
+  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(rc));
+  std::memcpy(id_out, &id, sizeof(id));
+  return PR_OK;
+}
+
+int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8_t *id) {
+  if (!g || !id) return fail(PR_ERR_INVALID, "NULL argument");
+  if (n_ranks != g->nparts || rank != g->part)
+    return fail(PR_ERR_INVALID, "rank/n_ranks must equal the graph's part/n_parts");
+  if (g->comm) return fail(PR_ERR_STATE, "communicator already attached");
+  DeviceGuard dg(g->device);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  ncclResult_t rc = ncclCommInitRank(&g->comm, n_ranks, uid, rank);
+  if (rc != ncclSuccess) {
+    g->comm = nullptr;
+    return fail(PR_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
+  }
+  g->comm_rank = rank;
+  g->comm_size = n_ranks;
+  return PR_OK;
+}
+
+void pr_graph_destroy(pr_graph *g) {
+  if (!g) return;
+  DeviceGuard dg(g->device);
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  if (g->comm) (void)ncclCommDestroy(g->comm);
+  for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
+  g->ev_pool.clear();
+  hipStream_t s = g->stream;
+  g->stream = nullptr;
+  delete g;  // DevBufs free their memory
+  if (s) (void)hipStreamDestroy(s);
+}
+
+}  // extern "C"

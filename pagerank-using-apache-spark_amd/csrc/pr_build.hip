@@ -1,0 +1,412 @@
+// Graph construction on the GPU (K1/K2 in SURVEY.md §2.1).
+//
+// Replaces Sparky.java:124-184:
+//   distinct().groupByKey()  (:124)      -> radix sort of (dst << b | src) keys + adjacent unique
+//   keys().collect/broadcast (:127-135)  -> PR_VF_KEY flag from the src column
+//   sink completion + union  (:137-161)  -> PR_VF_SINK = !KEY; every vertex is a row
+//   count()                  (:162)      -> N = n_vertices (all interned IDs must appear)
+//   dangUrls fixup           (:172-184)  -> D = sink-only vertices, resolved here once
+// then lays the part's rows out for the iteration (pr_graph.h) and plans the SpMV work units.
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "pr_compact.h"
+#include "pr_device.h"
+#include "pr_graph.h"
+
+namespace pr {
+namespace {
+
+constexpr uint64_t kSentinel = ~0ull;
+
+// ---- validation + key packing ----------------------------------------------------------
+__global__ void k_pack_edges(int64_t E, int32_t V, int b, const int32_t *__restrict__ src,
+                             const int32_t *__restrict__ dst, uint64_t *__restrict__ keys,
+                             uint8_t *__restrict__ appear, uint8_t *__restrict__ is_key,
+                             unsigned *__restrict__ err) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = src[i], d = dst[i];
+    if (s < 0 || s >= V || d < -1 || d >= V) {
+      atomicOr(err, 1u);
+      keys[i] = kSentinel;
+      continue;
+    }
+    appear[s] = 1;
+    is_key[s] = 1;
+    if (d >= 0) {
+      appear[d] = 1;
+      keys[i] = ((uint64_t)(uint32_t)d << b) | (uint32_t)s;
+    } else {
+      keys[i] = kSentinel;  // record without links: no edge (Sparky.java:114-118)
+    }
+  }
+}
+
+__global__ void k_check_appear(int32_t V, const uint8_t *__restrict__ appear, unsigned *err) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    if (!appear[v]) atomicOr(err, 2u);
+}
+
+struct UniquePred {
+  const uint64_t *k;
+  __device__ bool operator()(int64_t i) const {
+    const uint64_t x = k[i];
+    return x != kSentinel && (i == 0 || x != k[i - 1]);
+  }
+};
+struct IdentityU64 {
+  const uint64_t *k;
+  __device__ uint64_t operator()(int64_t i) const { return k[i]; }
+};
+
+// row_ptr[v] = first position whose row (key >> shift) is >= v; rows [0, R).
+__global__ void k_row_ptr(const uint64_t *__restrict__ keys, int64_t m, int shift, int64_t R,
+                          int64_t *__restrict__ row_ptr) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rc = (i < m) ? (int64_t)(keys[i] >> shift) : R;
+    const int64_t rp = (i > 0) ? (int64_t)(keys[i - 1] >> shift) : -1;
+    for (int64_t v = rp + 1; v <= rc; ++v) row_ptr[v] = i;
+  }
+}
+
+__global__ void k_canon_col_deg(const uint64_t *__restrict__ keys, int64_t m, uint64_t mask,
+                                int32_t *__restrict__ col, int32_t *__restrict__ deg) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = (int32_t)(keys[i] & mask);
+    col[i] = s;
+    atomicAdd(&deg[s], 1);
+  }
+}
+
+// vflags + global counters {n_sink, n_nolink, n_indeg0, max_indeg, max_outdeg}
+__global__ void k_vflags(int32_t V, const uint8_t *__restrict__ is_key,
+                         const int32_t *__restrict__ deg, const int64_t *__restrict__ row_ptr,
+                         uint8_t *__restrict__ vflags, unsigned long long *__restrict__ cnt) {
+  unsigned long long ns = 0, nn = 0, ni = 0;
+  unsigned long long mi = 0, mo = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t f = 0;
+    if (is_key[v]) {
+      f |= PR_VF_KEY;
+      if (deg[v] == 0) { f |= PR_VF_NOLINK; ++nn; }
+    } else {
+      f |= PR_VF_SINK;
+      ++ns;
+    }
+    const int64_t indeg = row_ptr[v + 1] - row_ptr[v];
+    if (indeg == 0) { f |= PR_VF_INDEG0; ++ni; }
+    vflags[v] = f;
+    mi = mi > (unsigned long long)indeg ? mi : (unsigned long long)indeg;
+    mo = mo > (unsigned long long)deg[v] ? mo : (unsigned long long)deg[v];
+  }
+  atomicAdd(&cnt[0], ns);
+  atomicAdd(&cnt[1], nn);
+  atomicAdd(&cnt[2], ni);
+  atomicMax(&cnt[3], mi);
+  atomicMax(&cnt[4], mo);
+}
+
+// Internal order key: out-degree descending, original ID ascending.
+__global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
+                             uint64_t *__restrict__ vk) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
+       v += (int64_t)gridDim.x * blockDim.x)
+    vk[v] = ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
+}
+
+// rank_of[v] = sorted index; gpos[v] = gather position of v's contribution.
+__global__ void k_rank_gpos(int32_t V, uint64_t mask, int P, int64_t S_pad,
+                            const uint64_t *__restrict__ sorted_vk, int32_t *__restrict__ rank_of,
+                            int32_t *__restrict__ gpos) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t v = (int32_t)(sorted_vk[i] & mask);
+    rank_of[v] = (int32_t)i;
+    gpos[v] = (int32_t)((i % P) * S_pad + i / P);
+  }
+}
+
+struct PartPred {
+  const uint64_t *k;
+  const int32_t *rank_of;
+  int b, P, part;
+  __device__ bool operator()(int64_t i) const {
+    const int32_t d = (int32_t)(k[i] >> b);
+    return rank_of[d] % P == part;
+  }
+};
+struct PartXform {
+  const uint64_t *k;
+  const int32_t *rank_of;
+  const int32_t *gpos;
+  int b, P, bg;
+  uint64_t mask;
+  __device__ uint64_t operator()(int64_t i) const {
+    const uint64_t key = k[i];
+    const int32_t d = (int32_t)(key >> b), s = (int32_t)(key & mask);
+    return ((uint64_t)(rank_of[d] / P) << bg) | (uint64_t)(uint32_t)gpos[s];
+  }
+};
+
+__global__ void k_local_col(const uint64_t *__restrict__ keys, int64_t m, uint64_t mask,
+                            int32_t *__restrict__ col) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
+       i += (int64_t)gridDim.x * blockDim.x)
+    col[i] = (int32_t)(keys[i] & mask);
+}
+
+__global__ void k_local_rows(int64_t n_local, int P, int part, uint64_t mask, bool dangling_none,
+                             const uint64_t *__restrict__ sorted_vk, const int32_t *__restrict__ deg,
+                             const uint8_t *__restrict__ vflags, int32_t *__restrict__ degf,
+                             int32_t *__restrict__ orig) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_local;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t v = (int32_t)(sorted_vk[j * P + part] & mask);
+    orig[j] = v;
+    const int32_t d = deg[v];
+    int32_t f = d;
+    if (d == 0) f = ((vflags[v] & PR_VF_SINK) && !dangling_none) ? -1 : 0;
+    degf[j] = f;
+  }
+}
+
+}  // namespace
+
+// Greedy work plan over the part's row_ptr (host; linear, deterministic).
+static void plan_units(const std::vector<int64_t> &rp, std::vector<Unit> &units,
+                       std::vector<int32_t> &lr_row, std::vector<int32_t> &lr_p0,
+                       int64_t *n_pieces) {
+  const int64_t R = (int64_t)rp.size() - 1;
+  int64_t pieces = 0;
+  int64_t v = 0;
+  units.clear();
+  lr_row.clear();
+  lr_p0.clear();
+  while (v < R) {
+    const int64_t len = rp[v + 1] - rp[v];
+    if (len > kUnitNnz) {
+      const int64_t np = (len + kUnitNnz - 1) / kUnitNnz;
+      lr_row.push_back((int32_t)v);
+      lr_p0.push_back((int32_t)pieces);
+      for (int64_t q = 0; q < np; ++q)
+        units.push_back(Unit{rp[v] + q * kUnitNnz, (int32_t)v, (int32_t)(-(pieces + q) - 1)});
+      pieces += np;
+      ++v;
+      continue;
+    }
+    const int64_t start = v;
+    int64_t nnz = 0;
+    while (v < R && v - start < kUnitRows) {
+      const int64_t l = rp[v + 1] - rp[v];
+      if (l > kUnitNnz || nnz + l > kUnitNnz) break;
+      nnz += l;
+      ++v;
+    }
+    units.push_back(Unit{rp[start], (int32_t)start, (int32_t)(v - start)});
+  }
+  lr_p0.push_back((int32_t)pieces);
+  *n_pieces = pieces;
+}
+
+int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
+  auto t_start = std::chrono::steady_clock::now();
+  hipStream_t s = g->stream;
+  const int32_t V = g->V;
+  const int P = g->nparts, part = g->part;
+  if (V < 0 || E < 0) return fail(PR_ERR_INVALID, "negative n_vertices or n_edges");
+  if (E >= (int64_t(1) << 32) - 1) return fail(PR_ERR_INVALID, "n_edges must be < 2^32 - 1");
+  const int b = bits_for((uint64_t)V);  // every ID < 2^b - 1: sentinel sorts last
+  const unsigned T = 256;
+
+  // ---- inputs on the device ----
+  DevBuf dsrc, ddst;
+  const int32_t *src = src_in, *dst = dst_in;
+  if (!(g->flags & PR_INPUT_DEVICE) && E > 0) {
+    PR_TRY(dsrc.alloc(sizeof(int32_t) * E));
+    PR_TRY(ddst.alloc(sizeof(int32_t) * E));
+    PR_HIP(hipMemcpyAsync(dsrc.p, src_in, sizeof(int32_t) * E, hipMemcpyHostToDevice, s));
+    PR_HIP(hipMemcpyAsync(ddst.p, dst_in, sizeof(int32_t) * E, hipMemcpyHostToDevice, s));
+    src = dsrc.as<int32_t>();
+    dst = ddst.as<int32_t>();
+  }
+
+  DevBuf keys, tmp, appear, is_key, err, cnt;
+  const int64_t Ealloc = E > 0 ? E : 1;
+  PR_TRY(keys.alloc(sizeof(uint64_t) * Ealloc));
+  PR_TRY(tmp.alloc(sizeof(uint64_t) * Ealloc));
+  PR_TRY(appear.alloc((size_t)V + 1));
+  PR_TRY(is_key.alloc((size_t)V + 1));
+  PR_TRY(err.alloc(sizeof(unsigned)));
+  PR_TRY(cnt.alloc(sizeof(unsigned long long) * 8));
+  PR_HIP(hipMemsetAsync(appear.p, 0, (size_t)V + 1, s));
+  PR_HIP(hipMemsetAsync(is_key.p, 0, (size_t)V + 1, s));
+  PR_HIP(hipMemsetAsync(err.p, 0, sizeof(unsigned), s));
+  PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long) * 8, s));
+  if (E > 0)
+    hipLaunchKernelGGL(k_pack_edges, dim3(grid_for(E, T, 65536)), dim3(T), 0, s, E, V, b, src, dst,
+                       keys.as<uint64_t>(), appear.as<uint8_t>(), is_key.as<uint8_t>(),
+                       err.as<unsigned>());
+  if (V > 0)
+    hipLaunchKernelGGL(k_check_appear, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V,
+                       appear.as<uint8_t>(), err.as<unsigned>());
+  PR_HIP(hipGetLastError());
+  unsigned herr = 0;
+  PR_HIP(hipMemcpyAsync(&herr, err.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  dsrc.reset();
+  ddst.reset();
+  appear.reset();
+  if (herr & 1u) return fail(PR_ERR_INVALID, "edge list holds an ID outside [0, n_vertices) (dst may be -1)");
+  if (herr & 2u) return fail(PR_ERR_INVALID, "an ID in [0, n_vertices) never appears in the edge list");
+
+  // ---- A1: sort + dedupe (Sparky.java:124) ----
+  PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), E, 0, 2 * b, s));
+  int64_t m = 0;
+  PR_TRY(compact_index(E, UniquePred{keys.as<uint64_t>()}, IdentityU64{keys.as<uint64_t>()},
+                       tmp.as<uint64_t>(), &m, s));
+  g->E_dedup = m;
+  uint64_t *ukeys = tmp.as<uint64_t>();
+  const uint64_t maskb = (uint64_t(1) << b) - 1;
+
+  // ---- canonical CSR, degrees, flags ----
+  DevBuf c_rowptr, c_col, c_deg, c_vflags;
+  PR_TRY(c_rowptr.alloc(sizeof(int64_t) * ((size_t)V + 1)));
+  PR_TRY(c_col.alloc(sizeof(int32_t) * (m > 0 ? m : 1)));
+  PR_TRY(c_deg.alloc(sizeof(int32_t) * ((size_t)V + 1)));
+  PR_TRY(c_vflags.alloc((size_t)V + 1));
+  PR_HIP(hipMemsetAsync(c_deg.p, 0, sizeof(int32_t) * ((size_t)V + 1), s));
+  hipLaunchKernelGGL(k_row_ptr, dim3(grid_for(m + 1, T, 65536)), dim3(T), 0, s, ukeys, m, b,
+                     (int64_t)V, c_rowptr.as<int64_t>());
+  if (m > 0)
+    hipLaunchKernelGGL(k_canon_col_deg, dim3(grid_for(m, T, 65536)), dim3(T), 0, s, ukeys, m, maskb,
+                       c_col.as<int32_t>(), c_deg.as<int32_t>());
+  if (V > 0)
+    hipLaunchKernelGGL(k_vflags, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, is_key.as<uint8_t>(),
+                       c_deg.as<int32_t>(), c_rowptr.as<int64_t>(), c_vflags.as<uint8_t>(),
+                       cnt.as<unsigned long long>());
+  PR_HIP(hipGetLastError());
+  unsigned long long hc[8] = {0};
+  PR_HIP(hipMemcpyAsync(hc, cnt.p, sizeof(hc), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  is_key.reset();
+  g->n_sink = (int64_t)hc[0];
+  g->n_nolink = (int64_t)hc[1];
+  g->n_indeg0 = (int64_t)hc[2];
+  g->max_indeg = (int64_t)hc[3];
+  const uint64_t max_outdeg = hc[4];
+
+  // ---- internal order: out-degree desc, ID asc (hot contributions first) ----
+  g->n_local_max = (V + P - 1) / P;
+  g->n_local = V > part ? (V - part + P - 1) / P : 0;
+  g->S_pad = ((g->n_local_max + 2 + 63) / 64) * 64;
+  const int bd = bits_for(max_outdeg);
+  const uint64_t maxd = (uint64_t(1) << bd) - 1;
+  DevBuf vk, vtmp, rank_of, gpos;
+  PR_TRY(vk.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
+  PR_TRY(vtmp.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
+  PR_TRY(rank_of.alloc(sizeof(int32_t) * ((size_t)V + 1)));
+  PR_TRY(gpos.alloc(sizeof(int32_t) * ((size_t)V + 1)));
+  if (V > 0) {
+    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, b, maxd,
+                       c_deg.as<int32_t>(), vk.as<uint64_t>());
+    PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd, s));
+    hipLaunchKernelGGL(k_rank_gpos, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, maskb, P,
+                       g->S_pad, vk.as<uint64_t>(), rank_of.as<int32_t>(), gpos.as<int32_t>());
+    PR_HIP(hipGetLastError());
+  }
+  vtmp.reset();
+
+  // ---- the part's in-link CSR in gather positions ----
+  const int bg = bits_for((uint64_t)P * g->S_pad);
+  const uint64_t maskg = (uint64_t(1) << bg) - 1;
+  int64_t lm = 0;
+  PR_TRY(compact_index(m, PartPred{ukeys, rank_of.as<int32_t>(), b, P, part},
+                       PartXform{ukeys, rank_of.as<int32_t>(), gpos.as<int32_t>(), b, P, bg, maskb},
+                       keys.as<uint64_t>(), &lm, s));
+  g->local_nnz = lm;
+  const int brow = bits_for((uint64_t)(g->n_local > 0 ? g->n_local : 1));
+  PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, 0, bg + brow, s));
+  PR_TRY(g->rowptr.alloc(sizeof(int64_t) * ((size_t)g->n_local + 1)));
+  PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 ? lm : 1)));
+  hipLaunchKernelGGL(k_row_ptr, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s, keys.as<uint64_t>(),
+                     lm, bg, g->n_local, g->rowptr.as<int64_t>());
+  if (lm > 0)
+    hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
+                       keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
+  PR_TRY(g->degf.alloc(sizeof(int32_t) * ((size_t)g->n_local + 1)));
+  DevBuf orig;
+  PR_TRY(orig.alloc(sizeof(int32_t) * ((size_t)g->n_local + 1)));
+  if (g->n_local > 0)
+    hipLaunchKernelGGL(k_local_rows, dim3(grid_for(g->n_local, T, 65536)), dim3(T), 0, s, g->n_local,
+                       P, part, maskb, (g->flags & PR_DANGLING_NONE) != 0, vk.as<uint64_t>(),
+                       c_deg.as<int32_t>(), c_vflags.as<uint8_t>(), g->degf.as<int32_t>(),
+                       orig.as<int32_t>());
+  PR_HIP(hipGetLastError());
+  keys.reset();
+  tmp.reset();
+  vk.reset();
+  rank_of.reset();
+  gpos.reset();
+
+  // ---- work plan (host greedy over the part's row_ptr) ----
+  std::vector<int64_t> rp((size_t)g->n_local + 1);
+  g->orig_of_local.resize((size_t)g->n_local);
+  PR_HIP(hipMemcpyAsync(rp.data(), g->rowptr.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
+  if (g->n_local > 0)
+    PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * g->n_local,
+                          hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  std::vector<Unit> hu;
+  std::vector<int32_t> hlr, hp0;
+  plan_units(rp, hu, hlr, hp0, &g->n_pieces);
+  g->n_units = (int64_t)hu.size();
+  g->n_long = (int64_t)hlr.size();
+  PR_TRY(g->units.alloc(sizeof(Unit) * (hu.size() + 1)));
+  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * (hu.size() + 1)));
+  PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (hlr.size() + 1)));
+  PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (hp0.size() + 1)));
+  PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
+  if (!hu.empty())
+    PR_HIP(hipMemcpyAsync(g->units.p, hu.data(), sizeof(Unit) * hu.size(), hipMemcpyHostToDevice, s));
+  if (!hlr.empty())
+    PR_HIP(hipMemcpyAsync(g->lr_row.p, hlr.data(), sizeof(int32_t) * hlr.size(), hipMemcpyHostToDevice, s));
+  PR_HIP(hipMemcpyAsync(g->lr_p0.p, hp0.data(), sizeof(int32_t) * hp0.size(), hipMemcpyHostToDevice, s));
+
+  // ---- iteration state ----
+  PR_TRY(g->r.alloc(sizeof(double) * ((size_t)g->n_local + 1)));
+  for (int k = 0; k < 2; ++k) {
+    PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)P * g->S_pad));
+    PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)P * g->S_pad, s));
+  }
+  g->fin_blocks = 512;
+  PR_TRY(g->fin_part.alloc(sizeof(double) * 2 * g->fin_blocks));
+  PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
+  PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
+  g->reset_blocks = (int)grid_for(g->n_local > 0 ? g->n_local : 1, 256, 2048);
+  PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
+
+  if (g->flags & PR_NO_CANONICAL) {
+    c_rowptr.reset();
+    c_col.reset();
+    c_deg.reset();
+    c_vflags.reset();
+    g->has_canonical = false;
+  } else {
+    g->canon_rowptr = std::move(c_rowptr);
+    g->canon_col = std::move(c_col);
+    g->canon_deg = std::move(c_deg);
+    g->canon_vflags = std::move(c_vflags);
+    g->has_canonical = true;
+  }
+  PR_HIP(hipStreamSynchronize(s));
+  g->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  return PR_OK;
+}
+
+}  // namespace pr

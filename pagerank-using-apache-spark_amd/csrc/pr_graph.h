@@ -1,0 +1,81 @@
+// The pr_graph handle: device-resident graph of one part plus iteration state.
+//
+// HBM layout of one part (DESIGN.md "Data layout"):
+//   internal vertex order   vertices sorted by (out-degree desc, original ID asc); sorted index
+//                           i is owned by part i % P as local row i / P.  Hot sources (high
+//                           out-degree = most-gathered contribution) sit together at the front.
+//   gather space            P slices of S_pad doubles; slice p = contributions c of part p's
+//                           rows, then two slots {dangling partial, L1 partial}.  col_idx holds
+//                           positions in this space, so the RCCL all-gather of the slices is
+//                           the whole exchange (one call per iteration).
+//   rowptr  int64[n_local+1]  in-link CSR of the part's rows (local row order)
+//   col     int32[nnz]        gather positions, ascending within a row
+//   degf    int32[n_local]    out-degree d>0; 0 = key without links; -1 = sink-only (in D)
+//   r       fp64[n_local]     ranks, updated in place
+//   cbuf    fp64[2][P*S_pad]  contributions r/d, double-buffered across iterations
+#pragma once
+
+#include <rccl/rccl.h>
+
+#include <vector>
+
+#include "pr_internal.h"
+
+struct pr_graph {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t flags = 0;
+
+  int32_t V = 0;          // N = totalUrlCount
+  int64_t E_dedup = 0;    // E'
+  int part = 0, nparts = 1;
+  int64_t n_local = 0;      // rows owned
+  int64_t n_local_max = 0;  // ceil(V / P)
+  int64_t S_pad = 0;        // doubles per gather slice
+  int64_t local_nnz = 0;
+
+  int64_t n_sink = 0, n_nolink = 0, n_indeg0 = 0, max_indeg = 0;
+  int64_t n_units = 0, n_long = 0, n_pieces = 0;
+  double build_ms = 0.0;
+
+  // canonical CSR in original IDs (kept unless PR_NO_CANONICAL)
+  pr::DevBuf canon_rowptr, canon_col, canon_deg, canon_vflags;
+  bool has_canonical = false;
+
+  // part layout
+  pr::DevBuf rowptr, col, degf, r;
+  pr::DevBuf cbuf[2];
+  pr::DevBuf units, unit_part;
+  pr::DevBuf lr_row, lr_p0, piece_part;
+  pr::DevBuf fin_part, fin_counter;
+  pr::DevBuf reset_part;
+  int fin_blocks = 0;
+  int reset_blocks = 0;
+  std::vector<int32_t> orig_of_local;  // host copy: local row -> original ID
+
+  // run state
+  double teleport = 0.15, damping = 0.85;
+  int cur = 0;  // cbuf[cur] holds the contributions of the current ranks
+  int64_t iters_done = 0;
+  bool ready = false;  // pr_reset was called
+
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;  // indices into ev_pool
+  size_t ev_next = 0;
+
+  // RCCL (one process per GPU)
+  ncclComm_t comm = nullptr;
+  int comm_rank = 0, comm_size = 1;
+
+  size_t device_bytes() const;
+};
+
+namespace pr {
+int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
+int iter_reset(pr_graph *g, const double *init_ranks_host);
+int iter_step(pr_graph *g, int32_t iterations);
+int exchange(pr_graph *g, int buf);
+int read_slots(pr_graph *g, int buf, double *dc, double *l1);
+}  // namespace pr

@@ -1,0 +1,90 @@
+// Internal declarations shared by the libpagerank_hip translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "pagerank_hip.h"
+
+namespace pr {
+
+// ---- error plumbing ---------------------------------------------------------------------
+void set_error(const std::string &msg);
+struct Status {
+  int code = PR_OK;
+  bool ok() const { return code == PR_OK; }
+};
+int fail(int code, const std::string &msg);
+
+#define PR_HIP(call)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return ::pr::fail(e_ == hipErrorOutOfMemory ? PR_ERR_OOM : PR_ERR_HIP,                  \
+                        std::string(#call) + ": " + hipGetErrorString(e_));                   \
+  } while (0)
+
+#define PR_TRY(expr)                                                                          \
+  do {                                                                                        \
+    int rc_ = (expr);                                                                         \
+    if (rc_ != PR_OK) return rc_;                                                             \
+  } while (0)
+
+// ---- device buffer (owning) ---------------------------------------------------------------
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    if (this != &o) { reset(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+    return *this;
+  }
+  ~DevBuf() { reset(); }
+  int alloc(size_t n);  // frees any previous allocation
+  void reset();
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// ---- primitives (pr_sort.hip) ---------------------------------------------------------------
+// Stable LSD radix sort of n u64 keys on bits [begin_bit, end_bit).  `tmp` must hold n keys.
+// The sorted result is left in `keys`.
+int radix_sort_u64(uint64_t *keys, uint64_t *tmp, int64_t n, int begin_bit, int end_bit,
+                   hipStream_t s);
+
+// Number of bits needed so that every value in [0, v] fits (v >= 0).
+inline int bits_for(uint64_t v) {
+  int b = 1;
+  while (b < 64 && (uint64_t(1) << b) <= v) ++b;
+  return b;
+}
+
+inline unsigned grid_for(int64_t n, int threads, unsigned cap = 1u << 20) {
+  int64_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ---- SpMV work plan ------------------------------------------------------------------------
+// A unit is one workgroup of the SpMV launch.  STREAM: whole rows [r0, r0+meta) whose in-links
+// total <= kUnitNnz.  PIECE: kUnitNnz in-links of one long row r0 starting at e0; meta =
+// -(piece index + 1).
+constexpr int kThreads = 256;       // workgroup size of the SpMV kernels (4 waves)
+constexpr int kPerThread = 8;       // in-links gathered per thread per unit
+constexpr int kUnitNnz = kThreads * kPerThread;  // 2048
+constexpr int kUnitRows = 1024;     // max rows per STREAM unit (LDS bound)
+
+struct Unit {
+  int64_t e0;
+  int32_t r0;
+  int32_t meta;
+};
+static_assert(sizeof(Unit) == 16, "Unit must stay 16 bytes");
+
+}  // namespace pr

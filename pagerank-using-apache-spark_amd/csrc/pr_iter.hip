@@ -1,0 +1,402 @@
+// The PageRank power iteration on gfx950 (K3/K4 in SURVEY.md §2.1): the hot path.
+//
+// One iteration of Sparky.java:189-235 is two launches plus, for several parts, one RCCL
+// all-gather:
+//
+//   k_spmv_units (one workgroup per work unit; THE dominant kernel)
+//     STREAM unit: whole rows [r0, r0+nr) with <= 2048 in-links.  The in-link column stream is
+//       read coalesced (int32), each lane gathers 8 contributions c[u] = r(u)/d(u) into LDS
+//       (Sparky.java:192-216 join + flatMapToPair), then every thread reduces 8 consecutive
+//       LDS values along row boundaries with a wave64 segmented scan for rows that cross
+//       threads (reduceByKey(Sum), Sparky.java:27-32, :229) -- balanced whatever the row
+//       lengths.  The epilogue is coalesced over the unit's rows and fuses:
+//         in-degree-0 quirk: S = r_old              (subtractByKey + union, :224-225)
+//         r' = 0.15 + 0.85 * (S + dc / N)           (:233, no FMA contraction)
+//         c' = r' / d for the next iteration        (:207, a true division)
+//         partial sum of r' over sink-only rows     (danglingContrib of the next iteration, :219-222)
+//         partial L1 |r' - r|                        (convergence norm; reported only)
+//     PIECE unit: 2048 in-links of a long row -> one partial sum.
+//   k_finalize: long rows (sum of their pieces in piece order + the same epilogue), then a
+//     deterministic reduction of all unit partials into the two slots {dc partial, L1 partial}
+//     at the end of this part's gather slice (last-arriving workgroup, agent-scope sc1 protocol
+//     of cdna_hip_programming.md Guideline 16).
+//
+// Every sum has a fixed order, so results are bitwise reproducible run to run.
+#include <climits>
+
+#include "pr_device.h"
+#include "pr_graph.h"
+
+namespace pr {
+namespace {
+
+__device__ __forceinline__ double dc_from_slots(const double *cin, int P, int64_t S_pad) {
+  double dc = 0.0;
+  for (int p = 0; p < P; ++p) dc = __dadd_rn(dc, cin[(int64_t)p * S_pad + S_pad - 2]);
+  return dc;
+}
+
+// r' = teleport + damping * (S + tdc), evaluated exactly as Sparky.java:233 (no contraction).
+__device__ __forceinline__ double affine(double S, double tdc, double teleport, double damping) {
+  return __dadd_rn(teleport, __dmul_rn(damping, __dadd_rn(S, tdc)));
+}
+
+__global__ __launch_bounds__(kThreads) void k_spmv_units(
+    const Unit *__restrict__ units, const int64_t *__restrict__ rowptr,
+    const int32_t *__restrict__ col, const double *__restrict__ cin, double *__restrict__ cout,
+    double *__restrict__ r, const int32_t *__restrict__ degf, double *__restrict__ piece_part,
+    double2 *__restrict__ unit_part, int P, int64_t S_pad, double n_vertices, double teleport,
+    double damping) {
+  __shared__ double val[kUnitNnz];
+  __shared__ double rowsum[kUnitRows];
+  __shared__ int32_t lrp[kUnitRows + 1];
+  __shared__ double red[kThreads / kWave];
+  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
+  __shared__ double wval_last[kThreads / kWave];
+
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const Unit u = units[blockIdx.x];
+
+  if (u.meta < 0) {  // ---- PIECE of a long row ----
+    const int64_t row_end = rowptr[u.r0 + 1];
+    int64_t n = row_end - u.e0;
+    if (n > kUnitNnz) n = kUnitNnz;
+    int32_t ci[kPerThread];
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      const int i = j * kThreads + t;
+      ci[j] = (i < n) ? col[u.e0 + i] : -1;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j)
+      if (ci[j] >= 0) acc = __dadd_rn(acc, cin[ci[j]]);
+    acc = block_sum<kThreads>(acc, red);
+    if (t == 0) {
+      piece_part[-u.meta - 1] = acc;
+      unit_part[blockIdx.x] = make_double2(0.0, 0.0);
+    }
+    return;
+  }
+
+  // ---- STREAM unit ----
+  const int nr = u.meta;
+  const int32_t r0 = u.r0;
+  const int64_t e0 = u.e0;
+  const int n = (int)(rowptr[r0 + nr] - e0);
+  for (int k = t; k <= nr; k += kThreads) lrp[k] = (int32_t)(rowptr[r0 + k] - e0);
+  {
+    int32_t ci[kPerThread];
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      const int i = j * kThreads + t;
+      ci[j] = (i < n) ? col[e0 + i] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kPerThread; ++j) {
+      const int i = j * kThreads + t;
+      if (ci[j] >= 0) val[i] = cin[ci[j]];
+    }
+  }
+  const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+  __syncthreads();
+
+  // Each thread reduces LDS elements [i0, i0+8) along row boundaries.
+  const int i0 = t * kPerThread;
+  int carry_row = -1, first_row = -1;
+  double carry_val = 0.0, first_sum = 0.0;
+  if (i0 < n) {
+    int lo = 0, hi = nr + 1;  // first k with lrp[k] > i0
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lrp[mid] <= i0) lo = mid + 1;
+      else hi = mid;
+    }
+    int cur = lo - 1;
+    const int kstart = cur;
+    const bool started_before = lrp[cur] < i0;
+    int next_end = lrp[cur + 1];
+    const int iend = (i0 + kPerThread < n) ? i0 + kPerThread : n;
+    double acc = 0.0;
+    bool open = false;
+    for (int i = i0; i < iend; ++i) {
+      acc = __dadd_rn(acc, val[i]);
+      open = true;
+      if (i + 1 == next_end) {
+        if (cur == kstart && started_before) {
+          first_row = cur;
+          first_sum = acc;
+        } else {
+          rowsum[cur] = acc;
+        }
+        acc = 0.0;
+        open = false;
+        ++cur;
+        while (cur < nr && lrp[cur + 1] == lrp[cur]) ++cur;  // skip in-degree-0 rows
+        next_end = (cur < nr) ? lrp[cur + 1] : INT_MAX;
+      }
+    }
+    if (open) {
+      carry_row = cur;
+      carry_val = acc;
+    }
+  }
+
+  // Segmented inclusive scan of (carry_row, carry_val) over threads.  Equal rows are
+  // contiguous in thread order, so a Hillis-Steele step may add the partner's value when the
+  // partner carries the same row.
+  int srow = carry_row;
+  double sval = carry_val;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int prow = __shfl_up(srow, off, kWave);
+    const double pval = __shfl_up(sval, off, kWave);
+    if (lane >= off && srow >= 0 && prow == srow) sval = __dadd_rn(pval, sval);
+  }
+  const int lane0_row = __shfl(carry_row, 0, kWave);
+  if (lane == kWave - 1) {
+    wrow_last[w] = srow;
+    wval_last[w] = sval;
+    wrow_first[w] = lane0_row;
+  }
+  __syncthreads();
+  // carry-in from earlier waves (serial over <= 3 waves, identical in every lane)
+  int prow_in = -1;
+  double pval_in = 0.0;
+  for (int ww = 0; ww < w; ++ww) {
+    const int rl = wrow_last[ww];
+    const bool full = (rl >= 0) && (wrow_first[ww] == rl);
+    if (full && prow_in == rl) pval_in = __dadd_rn(pval_in, wval_last[ww]);
+    else {
+      prow_in = rl;
+      pval_in = (rl >= 0) ? wval_last[ww] : 0.0;
+    }
+  }
+  // extend this wave's leading segment with the carry-in
+  if (srow >= 0 && srow == prow_in && lane0_row == srow) sval = __dadd_rn(pval_in, sval);
+  // exclusive value seen by thread t = inclusive value of thread t-1
+  int erow = __shfl_up(srow, 1, kWave);
+  double eval = __shfl_up(sval, 1, kWave);
+  if (lane == 0) {
+    erow = prow_in;
+    eval = pval_in;
+  }
+  if (first_row >= 0) rowsum[first_row] = (erow == first_row) ? __dadd_rn(eval, first_sum) : first_sum;
+  __syncthreads();
+
+  // Epilogue over the unit's rows (coalesced).
+  double dcp = 0.0, l1p = 0.0;
+  for (int k = t; k < nr; k += kThreads) {
+    const int64_t v = (int64_t)r0 + k;
+    const double rold = r[v];
+    const double S = (lrp[k + 1] > lrp[k]) ? rowsum[k] : rold;
+    const double rn = affine(S, tdc, teleport, damping);
+    r[v] = rn;
+    const int32_t df = degf[v];
+    if (df > 0) cout[v] = __ddiv_rn(rn, (double)df);
+    else if (df < 0) dcp = __dadd_rn(dcp, rn);
+    l1p = __dadd_rn(l1p, fabs(rn - rold));
+  }
+  dcp = block_sum<kThreads>(dcp, red);
+  l1p = block_sum<kThreads>(l1p, red);
+  if (t == 0) unit_part[blockIdx.x] = make_double2(dcp, l1p);
+}
+
+__device__ __forceinline__ void store_sc1(double *p, double x) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(x),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double *p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(kThreads) void k_finalize(
+    int64_t n_long, const int32_t *__restrict__ lr_row, const int32_t *__restrict__ lr_p0,
+    const double *__restrict__ piece_part, const double2 *__restrict__ parts, int64_t n_parts,
+    double *__restrict__ r, const int32_t *__restrict__ degf, const double *__restrict__ cin,
+    double *__restrict__ cout, int P, int64_t S_pad, double n_vertices, double teleport,
+    double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
+    double *__restrict__ slot_out) {
+  __shared__ double red[kThreads / kWave];
+  __shared__ int is_last;
+  const int t = threadIdx.x, lane = lane_id();
+  double dcp = 0.0, l1p = 0.0;
+  if (n_long > 0) {
+    const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+    const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
+    for (int64_t q = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); q < n_long; q += nw) {
+      const int32_t p0 = lr_p0[q], np = lr_p0[q + 1] - p0;
+      double acc = 0.0;
+      for (int k = lane; k < np; k += kWave) acc = __dadd_rn(acc, piece_part[p0 + k]);
+      acc = wave_sum(acc);
+      if (lane == 0) {
+        const int32_t v = lr_row[q];
+        const double rold = r[v];
+        const double rn = affine(acc, tdc, teleport, damping);
+        r[v] = rn;
+        const int32_t df = degf[v];
+        if (df > 0) cout[v] = __ddiv_rn(rn, (double)df);
+        else if (df < 0) dcp = __dadd_rn(dcp, rn);
+        l1p = __dadd_rn(l1p, fabs(rn - rold));
+      }
+    }
+  }
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + t; i < n_parts; i += (int64_t)gridDim.x * kThreads) {
+    const double2 pv = parts[i];
+    dcp = __dadd_rn(dcp, pv.x);
+    l1p = __dadd_rn(l1p, pv.y);
+  }
+  dcp = block_sum<kThreads>(dcp, red);
+  l1p = block_sum<kThreads>(l1p, red);
+  if (t == 0) {
+    store_sc1(&fin_part[2 * blockIdx.x], dcp);
+    store_sc1(&fin_part[2 * blockIdx.x + 1], l1p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == gridDim.x - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!is_last) return;
+  double a = 0.0, b = 0.0;
+  for (int i = t; i < (int)gridDim.x; i += kThreads) {
+    a = __dadd_rn(a, load_sc1(&fin_part[2 * i]));
+    b = __dadd_rn(b, load_sc1(&fin_part[2 * i + 1]));
+  }
+  a = block_sum<kThreads>(a, red);
+  b = block_sum<kThreads>(b, red);
+  if (t == 0) {
+    slot_out[0] = a;
+    slot_out[1] = b;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_reset(int64_t n_local, const double *__restrict__ init,
+                                                    double *__restrict__ r,
+                                                    const int32_t *__restrict__ degf,
+                                                    double *__restrict__ cout,
+                                                    double2 *__restrict__ parts) {
+  __shared__ double red[kThreads / kWave];
+  double dcp = 0.0;
+  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < n_local;
+       j += (int64_t)gridDim.x * kThreads) {
+    const double x = init ? init[j] : 1.0;  // Sparky.java:165-170
+    r[j] = x;
+    const int32_t df = degf[j];
+    if (df > 0) cout[j] = __ddiv_rn(x, (double)df);
+    else if (df < 0) dcp = __dadd_rn(dcp, x);
+  }
+  dcp = block_sum<kThreads>(dcp, red);
+  if (threadIdx.x == 0) parts[blockIdx.x] = make_double2(dcp, 0.0);
+}
+
+hipEvent_t next_event(pr_graph *g) {
+  if (g->ev_next >= g->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    g->ev_pool.push_back(e);
+  }
+  return g->ev_pool[g->ev_next++];
+}
+
+int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n_parts, int in_buf,
+                    int out_buf) {
+  const int64_t own = (int64_t)g->part * g->S_pad;
+  double *cout = g->cbuf[out_buf].as<double>() + own;
+  hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, g->stream, n_long,
+                     g->lr_row.as<int32_t>(), g->lr_p0.as<int32_t>(), g->piece_part.as<double>(),
+                     parts, n_parts, g->r.as<double>(), g->degf.as<int32_t>(),
+                     g->cbuf[in_buf].as<double>(), cout, g->nparts, g->S_pad, (double)g->V,
+                     g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
+                     cout + g->S_pad - 2);
+  PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+
+}  // namespace
+
+int iter_reset(pr_graph *g, const double *init_host) {
+  hipStream_t s = g->stream;
+  DevBuf dinit;
+  if (init_host && g->n_local > 0) {
+    std::vector<double> loc((size_t)g->n_local);
+    for (int64_t j = 0; j < g->n_local; ++j) loc[j] = init_host[g->orig_of_local[j]];
+    PR_TRY(dinit.alloc(sizeof(double) * g->n_local));
+    PR_HIP(hipMemcpyAsync(dinit.p, loc.data(), sizeof(double) * g->n_local, hipMemcpyHostToDevice, s));
+    PR_HIP(hipStreamSynchronize(s));
+  }
+  g->cur = 0;
+  const int64_t own = (int64_t)g->part * g->S_pad;
+  hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_local,
+                     dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->degf.as<int32_t>(),
+                     g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
+  PR_HIP(hipGetLastError());
+  PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0));
+  PR_TRY(exchange(g, 0));
+  PR_HIP(hipStreamSynchronize(s));
+  g->iters_done = 0;
+  g->ready = true;
+  g->ev_next = 0;
+  g->spmv_ev.clear();
+  g->iter_ev.clear();
+  g->xchg_ev.clear();
+  return PR_OK;
+}
+
+int iter_step(pr_graph *g, int32_t iterations) {
+  if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
+  hipStream_t s = g->stream;
+  const int64_t own = (int64_t)g->part * g->S_pad;
+  for (int32_t it = 0; it < iterations; ++it) {
+    const int in = g->cur, out = g->cur ^ 1;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    if (g->timing) {
+      e0 = next_event(g);
+      e1 = next_event(g);
+      e2 = next_event(g);
+      e3 = next_event(g);
+      if (!e0 || !e1 || !e2 || !e3) return fail(PR_ERR_HIP, "hipEventCreate failed");
+      PR_HIP(hipEventRecord(e0, s));
+    }
+    if (g->n_units > 0)
+      hipLaunchKernelGGL(k_spmv_units, dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
+                         g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->col.as<int32_t>(),
+                         g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
+                         g->degf.as<int32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
+                         g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping);
+    PR_HIP(hipGetLastError());
+    if (g->timing) PR_HIP(hipEventRecord(e1, s));
+    PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units, in, out));
+    if (g->timing) PR_HIP(hipEventRecord(e2, s));
+    PR_TRY(exchange(g, out));
+    if (g->timing) {
+      PR_HIP(hipEventRecord(e3, s));
+      const int base = (int)g->ev_next - 4;
+      g->spmv_ev.push_back({base, base + 1});
+      g->xchg_ev.push_back({base + 2, base + 3});
+      g->iter_ev.push_back({base, base + 3});
+    }
+    g->cur = out;
+    ++g->iters_done;
+  }
+  return PR_OK;
+}
+
+int read_slots(pr_graph *g, int buf, double *dc, double *l1) {
+  std::vector<double> h(2 * (size_t)g->nparts);
+  for (int p = 0; p < g->nparts; ++p)
+    PR_HIP(hipMemcpyAsync(&h[2 * p], g->cbuf[buf].as<double>() + (int64_t)p * g->S_pad + g->S_pad - 2,
+                          2 * sizeof(double), hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  double a = 0.0, b = 0.0;
+  for (int p = 0; p < g->nparts; ++p) {
+    a += h[2 * p];
+    b += h[2 * p + 1];
+  }
+  *dc = a;
+  *l1 = b;
+  return PR_OK;
+}
+
+}  // namespace pr

@@ -1,0 +1,105 @@
+"""ctypes binding of libpagerank_hip (include/pagerank_hip.h).
+
+This is what a Python host binds; the JVM host binds the same symbols through Panama FFM or
+JNI.  The library is loaded from the in-tree build directory; there is no
+fallback -- a missing or unloadable library raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+BUILD_DIR = os.path.join(os.path.dirname(_PKG_DIR), "build")
+LIB_PATH = os.path.join(BUILD_DIR, "libpagerank_hip.so")
+
+PR_OK = 0
+PR_ERR_INVALID = -1
+PR_ERR_HIP = -2
+PR_ERR_OOM = -3
+PR_ERR_COMM = -4
+PR_ERR_STATE = -5
+PR_ERR_NODEVICE = -6
+
+PR_DANGLING_LOCAL = 0
+PR_DANGLING_NONE = 1
+PR_INPUT_DEVICE = 2
+PR_NO_CANONICAL = 4
+
+PR_VF_KEY, PR_VF_SINK, PR_VF_NOLINK, PR_VF_INDEG0 = 1, 2, 4, 8
+
+INFO_NAMES = ["n_vertices", "n_edges", "n_sink", "n_nolink", "n_indeg0", "max_indeg", "local_rows",
+              "local_edges", "part", "n_parts", "n_units", "n_long_rows", "device_bytes"]
+STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "iter_ms_mean",
+              "build_ms", "exchange_ms_mean"]
+PR_CB_RANKS = 1
+PR_COMM_ID_BYTES = 128
+
+# Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "pr_abi_version", "pr_last_error", "pr_device_count", "pr_graph_create", "pr_graph_create_part",
+    "pr_graph_info", "pr_graph_export_csr", "pr_run", "pr_reset", "pr_step", "pr_sync",
+    "pr_get_ranks", "pr_set_timing", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
+    "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_intern_device",
+]
+
+ITER_CB = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_double,
+                           ctypes.c_double, ctypes.c_double, ctypes.c_void_p)
+
+
+class PageRankError(RuntimeError):
+    """A non-zero status from libpagerank_hip (the JVM shim maps it to RuntimeException)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libpagerank_hip error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(
+            f"{LIB_PATH} is missing: build it with `make -C pagerank-using-apache-spark_amd/csrc` "
+            "or `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    i32, i64, u32, u64, dbl = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double
+    sig = {
+        "pr_abi_version": ([], ctypes.c_int),
+        "pr_last_error": ([], ctypes.c_char_p),
+        "pr_device_count": ([P], ctypes.c_int),
+        "pr_graph_create": ([i32, i32, i64, P, P, u32, P], ctypes.c_int),
+        "pr_graph_create_part": ([i32, i32, i32, i32, i64, P, P, u32, P], ctypes.c_int),
+        "pr_graph_info": ([P, P, i32], ctypes.c_int),
+        "pr_graph_export_csr": ([P, P, P, P, P], ctypes.c_int),
+        "pr_run": ([P, i32, dbl, dbl, P, P, ITER_CB, u32, P], ctypes.c_int),
+        "pr_reset": ([P, dbl, dbl, P], ctypes.c_int),
+        "pr_step": ([P, i32], ctypes.c_int),
+        "pr_sync": ([P], ctypes.c_int),
+        "pr_get_ranks": ([P, P], ctypes.c_int),
+        "pr_set_timing": ([P, i32], ctypes.c_int),
+        "pr_get_stats": ([P, P, i32], ctypes.c_int),
+        "pr_comm_unique_id": ([P], ctypes.c_int),
+        "pr_graph_attach_comm": ([P, i32, i32, P], ctypes.c_int),
+        "pr_graph_destroy": ([P], None),
+        "pr_gen_rmat": ([i32, i32, i64, dbl, dbl, dbl, u64, P, P], ctypes.c_int),
+        "pr_gen_er": ([i32, i32, i64, u64, P, P], ctypes.c_int),
+        "pr_intern_device": ([i32, i64, i32, P, P, P], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != PR_OK:
+        msg = load().pr_last_error()
+        raise PageRankError(rc, msg.decode() if msg else "")

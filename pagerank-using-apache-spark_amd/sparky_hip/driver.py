@@ -1,0 +1,157 @@
+"""Process-level drop-in for the Spark job (Python host; the C++ CLI ``pagerank`` is the same).
+
+CLI: ``python -m sparky_hip <edge-list-path> [iterations=10] [--out DIR]
+[--save-every-iter] [--dangling=local|none] [--device N] [--quiet]``
+
+* input: text edge list, ``src dst`` per line; a single-token line ``src`` is a record without
+  ``a`` links (Sparky.java:114-118).  Tokens (URLs) are taken verbatim and interned to dense
+  int32 IDs in first-appearance order, src before dst.
+* stdout: ``Starting iter<i>`` before every iteration (Sparky.java:188), then
+  ``<url> has rank: <r>.`` for every URL after the last iteration (north_star contract).
+* ``--out DIR``: ``DIR/PageRank<i>/part-00000`` with ``(url,rank)`` lines -- Scala
+  ``Tuple2.toString`` of ``(String, Double)`` with Java ``Double.toString`` -- plus an empty
+  ``_SUCCESS`` (Sparky.java:237 ``saveAsTextFile``); only the last iteration unless
+  ``--save-every-iter``.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+from typing import Dict, Iterable, List, Sequence, TextIO, Tuple
+
+import numpy as np
+
+from .graph import PageRankGraph
+
+
+def java_double_to_string(x: float) -> str:
+    """``Double.toString`` (shortest-uniquely-distinguishing digits, JDK 19+ algorithm).
+
+    Layout per the JDK spec: decimal notation for 1e-3 <= |x| < 1e7 with at least one digit
+    after the point; otherwise ``d.dddE<exp>``.  JDK <= 18 (Spark 1.x era) emits a longer,
+    non-shortest digit string for a few values (JDK-4511638); parity tests therefore compare
+    parsed numbers, never strings.
+    """
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0.0:
+        return "-0.0" if math.copysign(1.0, x) < 0 else "0.0"
+    sign = "-" if x < 0 else ""
+    ax = abs(x)
+    r = repr(ax)  # shortest round-trip digits
+    if "e" in r or "E" in r:
+        mant, exp = r.lower().split("e")
+        e10 = int(exp)
+    else:
+        mant, e10 = r, 0
+    if "." in mant:
+        ip, fp = mant.split(".")
+    else:
+        ip, fp = mant, ""
+    digits = (ip + fp).lstrip("0")
+    # position of the decimal point relative to the first significant digit
+    lead_zeros = len(ip + fp) - len((ip + fp).lstrip("0"))
+    point = len(ip) - lead_zeros + e10  # value = 0.digits * 10^point
+    digits = digits.rstrip("0") or "0"
+    if len(digits) == 1:
+        # JDK 19+ renders at least two significant digits and picks the 2-digit decimal
+        # closest to the value when the 1-digit shortest is not (e.g. 4.9E-324, not 5.0E-324).
+        m2, e2 = f"{ax:.1e}".split("e")
+        d2 = m2.replace(".", "").rstrip("0") or "0"
+        digits, point = d2, int(e2) + 1
+    if 1e-3 <= ax < 1e7:
+        if point <= 0:
+            s = "0." + "0" * (-point) + digits
+        elif point >= len(digits):
+            s = digits + "0" * (point - len(digits)) + ".0"
+        else:
+            s = digits[:point] + "." + digits[point:]
+        return sign + s
+    frac = digits[1:] or "0"
+    return f"{sign}{digits[0]}.{frac}E{point - 1}"
+
+
+def read_edge_list(lines: Iterable[str]) -> Tuple[List[str], np.ndarray, np.ndarray]:
+    """Tokenise and intern (first appearance, src before dst).  Returns (urls, src, dst)."""
+    ids: Dict[str, int] = {}
+    urls: List[str] = []
+    src: List[int] = []
+    dst: List[int] = []
+    for ln, line in enumerate(lines):
+        toks = line.split()
+        if not toks:
+            continue
+        if len(toks) > 2:
+            raise ValueError(f"line {ln + 1}: expected 'src [dst]', got {len(toks)} tokens")
+        u = toks[0]
+        iu = ids.get(u)
+        if iu is None:
+            iu = ids[u] = len(urls)
+            urls.append(u)
+        src.append(iu)
+        if len(toks) == 1:
+            dst.append(-1)
+        else:
+            v = toks[1]
+            iv = ids.get(v)
+            if iv is None:
+                iv = ids[v] = len(urls)
+                urls.append(v)
+            dst.append(iv)
+    return urls, np.asarray(src, np.int32), np.asarray(dst, np.int32)
+
+
+def write_part_file(out_dir: str, iteration: int, urls: Sequence[str], ranks: np.ndarray) -> str:
+    """``ranks.saveAsTextFile(out_dir + "/PageRank" + iter + "/")`` (Sparky.java:237)."""
+    d = os.path.join(out_dir, f"PageRank{iteration}")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "part-00000"), "w") as f:
+        for u, r in zip(urls, ranks.tolist()):
+            f.write(f"({u},{java_double_to_string(r)})\n")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+    return d
+
+
+def write_has_rank(stream: TextIO, urls: Sequence[str], ranks: np.ndarray) -> None:
+    for u, r in zip(urls, ranks.tolist()):
+        stream.write(f"{u} has rank: {java_double_to_string(r)}.\n")
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="sparky_hip", description=__doc__.splitlines()[0])
+    ap.add_argument("edge_list")
+    ap.add_argument("iterations", nargs="?", type=int, default=10)  # Sparky.java:187
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--save-every-iter", action="store_true")
+    ap.add_argument("--dangling", choices=["local", "none"], default="local")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--quiet", action="store_true", help="omit the '<url> has rank' lines")
+    a = ap.parse_args(argv)
+    with open(a.edge_list) as f:
+        urls, src, dst = read_edge_list(f)
+    out = sys.stdout
+    with PageRankGraph(len(urls), src, dst, device=a.device, dangling=a.dangling,
+                       keep_canonical=False) as g:
+        def cb(it, ranks, _st):
+            if a.out and (a.save_every_iter or it == a.iterations - 1):
+                write_part_file(a.out, it, urls, ranks)
+
+        # Sparky prints "Starting iter<i>" before each iteration (Sparky.java:188); the library
+        # calls back after iteration i, so the host prints the next line there.
+        def cb_print(it, ranks, st):
+            cb(it, ranks, st)
+            if it + 1 < a.iterations:
+                out.write(f"Starting iter{it + 1}\n")
+
+        if a.iterations > 0:
+            out.write("Starting iter0\n")
+        ranks, _ = g.run(a.iterations, callback=cb_print,
+                         want_ranks_in_callback=bool(a.out))
+    if not a.quiet:
+        write_has_rank(out, urls, ranks)
+    out.flush()
+    return 0

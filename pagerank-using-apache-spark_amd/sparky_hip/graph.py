@@ -1,0 +1,198 @@
+"""Python host mirror of the Sparky.java hot path on top of libpagerank_hip.
+
+``PageRankGraph`` owns one ``pr_graph`` handle.  Its methods map one-to-one to the reference's
+stages:
+
+* ``PageRankGraph(...)``       Sparky.java:124-184  (graph construction, N, dangling set)
+* ``run(iterations)``          Sparky.java:164-238  (rank init + the power iteration)
+* ``export_csr()``             the canonical in-link CSR, for bit-exact tests
+
+Device memory is owned by the library.  Host arrays passed in are borrowed for the call only.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+@dataclass
+class CanonicalCSR:
+    row_ptr: np.ndarray  # int64[V+1]
+    col_idx: np.ndarray  # int32[E']
+    out_deg: np.ndarray  # int32[V]
+    vflags: np.ndarray  # uint8[V]
+
+
+@dataclass
+class IterationStats:
+    iteration: int
+    dangling_sum: float
+    l1_delta: float
+    ms: float
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(_lib.load().pr_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class PageRankGraph:
+    """One part of the in-link graph resident on one GPU."""
+
+    def __init__(self, n_vertices: int, src, dst, *, device: int = 0, dangling: str = "local",
+                 part: int = 0, n_parts: int = 1, keep_canonical: bool = True,
+                 device_input: bool = False, n_edges: Optional[int] = None):
+        """src/dst: int32 host arrays (numpy) of raw interned edges, dst == -1 for a record
+        without links; or, with device_input=True, integer device addresses (e.g. from
+        torch ``tensor.data_ptr()``) plus n_edges."""
+        L = _lib.load()
+        flags = 0
+        if dangling == "none":
+            flags |= _lib.PR_DANGLING_NONE
+        elif dangling != "local":
+            raise ValueError("dangling must be 'local' or 'none'")
+        if not keep_canonical:
+            flags |= _lib.PR_NO_CANONICAL
+        if device_input:
+            flags |= _lib.PR_INPUT_DEVICE
+            if n_edges is None:
+                raise ValueError("n_edges is required with device_input=True")
+            ps, pd = ctypes.c_void_p(int(src)), ctypes.c_void_p(int(dst))
+            ne = int(n_edges)
+        else:
+            src = np.ascontiguousarray(src, dtype=np.int32)
+            dst = np.ascontiguousarray(dst, dtype=np.int32)
+            if src.shape != dst.shape:
+                raise ValueError("src and dst must have the same length")
+            ps, pd = _ptr(src), _ptr(dst)
+            ne = int(src.shape[0])
+        self._h = ctypes.c_void_p()
+        if n_parts == 1 and part == 0:
+            rc = L.pr_graph_create(device, int(n_vertices), ne, ps, pd, flags, ctypes.byref(self._h))
+        else:
+            rc = L.pr_graph_create_part(device, part, n_parts, int(n_vertices), ne, ps, pd, flags,
+                                        ctypes.byref(self._h))
+        check(rc)
+        self.n_vertices = int(n_vertices)
+        self.part, self.n_parts = part, n_parts
+
+    # -- lifecycle ---------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            _lib.load().pr_graph_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- queries -----------------------------------------------------------------------------
+    def info(self) -> dict:
+        a = np.zeros(len(_lib.INFO_NAMES), np.int64)
+        check(_lib.load().pr_graph_info(self._h, _ptr(a), len(a)))
+        return dict(zip(_lib.INFO_NAMES, (int(x) for x in a)))
+
+    def export_csr(self) -> CanonicalCSR:
+        inf = self.info()
+        V, E = inf["n_vertices"], inf["n_edges"]
+        rp = np.zeros(V + 1, np.int64)
+        col = np.zeros(max(E, 1), np.int32)
+        deg = np.zeros(max(V, 1), np.int32)
+        vf = np.zeros(max(V, 1), np.uint8)
+        check(_lib.load().pr_graph_export_csr(self._h, _ptr(rp), _ptr(col), _ptr(deg), _ptr(vf)))
+        return CanonicalCSR(rp, col[:E], deg[:V], vf[:V])
+
+    def stats(self) -> dict:
+        a = np.zeros(len(_lib.STAT_NAMES), np.float64)
+        check(_lib.load().pr_get_stats(self._h, _ptr(a), len(a)))
+        return dict(zip(_lib.STAT_NAMES, (float(x) for x in a)))
+
+    # -- iteration ---------------------------------------------------------------------------
+    def run(self, iterations: int = 10, *, teleport: float = 0.15, damping: float = 0.85,
+            init_ranks=None, callback: Optional[Callable] = None, want_ranks_in_callback: bool = False):
+        """Sparky.java:164-238.  Returns final ranks (float64[V], original-ID order) and the
+        per-iteration stats.  ``callback(iter, ranks_or_None, stats)`` runs between iterations."""
+        V = self.n_vertices
+        out = np.zeros(max(V, 1), np.float64)
+        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        history: List[IterationStats] = []
+
+        def _cb(it, rp, dc, l1, ms, _user):
+            st = IterationStats(int(it), float(dc), float(l1), float(ms))
+            history.append(st)
+            if callback is not None:
+                arr = np.ctypeslib.as_array(rp, shape=(V,)).copy() if rp else None
+                callback(int(it), arr, st)
+
+        cb = _lib.ITER_CB(_cb)
+        flags = _lib.PR_CB_RANKS if want_ranks_in_callback else 0
+        check(_lib.load().pr_run(self._h, int(iterations), teleport, damping, _ptr(init), _ptr(out),
+                                 cb, flags, None))
+        return out[:V], history
+
+    def reset(self, *, teleport: float = 0.15, damping: float = 0.85, init_ranks=None) -> None:
+        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        check(_lib.load().pr_reset(self._h, teleport, damping, _ptr(init)))
+
+    def step(self, iterations: int) -> None:
+        check(_lib.load().pr_step(self._h, int(iterations)))
+
+    def sync(self) -> None:
+        check(_lib.load().pr_sync(self._h))
+
+    def ranks(self, out: Optional[np.ndarray] = None) -> np.ndarray:
+        if out is None:
+            out = np.zeros(max(self.n_vertices, 1), np.float64)
+        check(_lib.load().pr_get_ranks(self._h, _ptr(out)))
+        return out[: self.n_vertices]
+
+    def set_timing(self, enable: bool) -> None:
+        check(_lib.load().pr_set_timing(self._h, 1 if enable else 0))
+
+    # -- multi-process -------------------------------------------------------------------------
+    def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:
+        buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES).from_buffer_copy(uid)
+        check(_lib.load().pr_graph_attach_comm(self._h, rank, n_ranks, buf))
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES)()
+    check(_lib.load().pr_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def gen_rmat(device: int, scale: int, n_edges: int, src_ptr: int, dst_ptr: int, *, a=0.57, b=0.19,
+             c=0.19, seed: int = 1) -> None:
+    check(_lib.load().pr_gen_rmat(device, scale, n_edges, a, b, c, seed, ctypes.c_void_p(src_ptr),
+                                  ctypes.c_void_p(dst_ptr)))
+
+
+def gen_er(device: int, scale: int, n_edges: int, src_ptr: int, dst_ptr: int, *, seed: int = 3) -> None:
+    check(_lib.load().pr_gen_er(device, scale, n_edges, seed, ctypes.c_void_p(src_ptr),
+                                ctypes.c_void_p(dst_ptr)))
+
+
+def intern_device(device: int, n_edges: int, label_bound: int, src_ptr: int, dst_ptr: int) -> int:
+    nv = ctypes.c_int32(0)
+    check(_lib.load().pr_intern_device(device, n_edges, label_bound, ctypes.c_void_p(src_ptr),
+                                       ctypes.c_void_p(dst_ptr), ctypes.byref(nv)))
+    return nv.value

@@ -1,0 +1,79 @@
+"""The C-ABI boundary on CPU: libpagerank_hip loads, exports every symbol include/pagerank_hip.h
+declares, and fails loudly (never falls back to a CPU path) when there is no GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def header_functions():
+    hdr = open(os.path.join(ROOT, "include", "pagerank_hip.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return sorted(set(re.findall(r"\b(pr_[a-z_]+)\s*\(", hdr)))
+
+
+def test_library_exports_every_declared_symbol():
+    import sparky_hip._lib as L
+
+    lib = L.load()
+    declared = header_functions()
+    assert len(declared) >= 20
+    missing = [f for f in declared if not hasattr(lib, f)]
+    assert missing == []
+    assert sorted(L.EXPORTED) == declared
+
+
+def test_abi_version():
+    import sparky_hip._lib as L
+
+    hdr = open(os.path.join(ROOT, "include", "pagerank_hip.h")).read()
+    ver = int(re.search(r"#define PR_ABI_VERSION (\d+)", hdr).group(1))
+    assert L.load().pr_abi_version() == ver
+
+
+def test_constants_match_header():
+    import sparky_hip._lib as L
+
+    hdr = open(os.path.join(ROOT, "include", "pagerank_hip.h")).read()
+    for name in ["PR_DANGLING_NONE", "PR_INPUT_DEVICE", "PR_NO_CANONICAL", "PR_VF_KEY", "PR_VF_SINK",
+                 "PR_VF_NOLINK", "PR_VF_INDEG0", "PR_CB_RANKS", "PR_COMM_ID_BYTES"]:
+        v = int(re.search(rf"#define {name} \(?(\d+)u?\)?", hdr).group(1))
+        assert getattr(L, name) == v, name
+    for name in ["PR_ERR_INVALID", "PR_ERR_HIP", "PR_ERR_OOM", "PR_ERR_COMM", "PR_ERR_STATE", "PR_ERR_NODEVICE"]:
+        v = int(re.search(rf"#define {name} \((-\d+)\)", hdr).group(1))
+        assert getattr(L, name) == v, name
+    n_info = int(re.search(r"#define PR_INFO_COUNT (\d+)", hdr).group(1))
+    n_stat = int(re.search(r"#define PR_STAT_COUNT (\d+)", hdr).group(1))
+    assert len(L.INFO_NAMES) == n_info and len(L.STAT_NAMES) == n_stat
+
+
+def _has_gpu():
+    import sparky_hip
+
+    return sparky_hip.device_count() > 0
+
+
+def test_no_gpu_fails_loudly():
+    import sparky_hip
+
+    if _has_gpu():
+        pytest.skip("GPU present: covered by the gpu tests")
+    with pytest.raises(sparky_hip.PageRankError) as ei:
+        sparky_hip.PageRankGraph(2, np.array([0], np.int32), np.array([1], np.int32))
+    assert ei.value.code == -6  # PR_ERR_NODEVICE
+    assert "device" in str(ei.value)
+
+
+def test_null_arguments_rejected():
+    import sparky_hip._lib as L
+
+    lib = L.load()
+    assert lib.pr_graph_info(None, None, 0) == L.PR_ERR_INVALID
+    assert lib.pr_step(None, 1) == L.PR_ERR_INVALID
+    assert lib.pr_device_count(None) == L.PR_ERR_INVALID
+    assert b"NULL" in lib.pr_last_error()
+    lib.pr_graph_destroy(None)  # no-op

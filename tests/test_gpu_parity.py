@@ -1,0 +1,246 @@
+"""GPU parity tests: libpagerank_hip (HIP, gfx950) against the oracles, through the C ABI.
+
+Bars (BASELINE.json north_star):
+* canonical CSR, out-degrees, vertex flags and the ID mapping: bit-exact;
+* ranks: max relative error <= 1e-9 after the same iteration count (RANK_TOL below) -- the
+  only freedom is summation order (Spark's reduceByKey order is unspecified).
+"""
+import numpy as np
+import pytest
+
+import sparky_rdd
+
+pytestmark = pytest.mark.gpu
+
+RANK_TOL = 1e-9  # north_star: "ranks within 1e-9 max relative error"
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import sparky_hip
+
+    assert sparky_hip.device_count() > 0, "no GPU visible: the gpu tests need an MI355X"
+    return sparky_hip
+
+
+def max_rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    if a.size == 0:
+        return 0.0
+    return float(np.max(np.abs(a - b) / np.abs(b)))
+
+
+def assert_csr_equal(g, csr):
+    ex = g.export_csr()
+    assert np.array_equal(ex.row_ptr, csr.row_ptr)
+    assert np.array_equal(ex.col_idx, csr.col_idx)
+    assert np.array_equal(ex.out_deg, csr.out_deg)
+    assert np.array_equal(ex.vflags, csr.vflags)
+
+
+def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None):
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
+    with hip.PageRankGraph(V, src, dst, dangling=dangling) as g:
+        assert_csr_equal(g, csr)
+        hist = []
+        ranks, stats = g.run(iters, init_ranks=init, want_ranks_in_callback=True,
+                             callback=lambda it, r, st: hist.append(r))
+        info = g.info()
+    return csr, ref, ranks, stats, hist, info
+
+
+def test_golden_fixtures(hip, golden_cases):
+    for c in golden_cases:
+        urls, src, dst = hip.read_edge_list(c["lines"])
+        assert urls == c["urls"]
+        with hip.PageRankGraph(len(urls), src, dst, dangling=c["dangling"]) as g:
+            assert g.info()["n_vertices"] == c["N"]
+            assert g.info()["n_sink"] == (c["n_dangling"] if c["dangling"] == "local" else g.info()["n_sink"])
+            hist = []
+            ranks, stats = g.run(c["iterations"], want_ranks_in_callback=True,
+                                 callback=lambda it, r, st: hist.append(r))
+        for it in range(c["iterations"]):
+            assert max_rel(hist[it], c["ranks"][it]) <= RANK_TOL, (c["name"], it)
+            want_dc = c["dc"][it]
+            assert abs(stats[it].dangling_sum - want_dc) <= RANK_TOL * max(abs(want_dc), 1.0), (c["name"], it)
+        assert np.array_equal(ranks, hist[-1])
+
+
+def test_kat_exact_values(hip):
+    urls, src, dst = hip.read_edge_list(["A B", "A C", "A B", "B C", "C A", "C C", "D", "E A", "E F"])
+    with hip.PageRankGraph(len(urls), src, dst) as g:
+        r, st = g.run(1)
+        inf = g.info()
+    assert inf["n_edges"] == 7 and inf["n_sink"] == 1 and inf["n_nolink"] == 1 and inf["n_indeg0"] == 2
+    want = dict(A=1.1416666666666666, B=0.7166666666666667, C=1.9916666666666665,
+                D=1.1416666666666666, E=1.1416666666666666, F=0.7166666666666667)
+    assert {u: float(x) for u, x in zip(urls, r)} == want
+
+
+def random_edges(rng, V, E, p_nolink=0.05, hub_frac=0.0):
+    src = rng.integers(0, V, E, dtype=np.int64)
+    dst = rng.integers(0, V, E, dtype=np.int64)
+    if hub_frac > 0:
+        h = rng.random(E) < hub_frac
+        dst[h] = 0
+    dst[rng.random(E) < p_nolink] = -1
+    # make every ID appear: append one edge per missing vertex
+    seen = np.zeros(V, bool)
+    seen[src] = True
+    seen[dst[dst >= 0]] = True
+    miss = np.nonzero(~seen)[0]
+    src = np.concatenate([src, miss])
+    dst = np.concatenate([dst, np.full(miss.shape, -1)])
+    return src.astype(np.int32), dst.astype(np.int32)
+
+
+@pytest.mark.parametrize("V,E,seed", [(1, 1, 0), (17, 60, 1), (1000, 9000, 2), (50000, 800000, 3)])
+def test_random_graphs(hip, oracle_c, V, E, seed):
+    rng = np.random.default_rng(seed)
+    src, dst = random_edges(rng, V, E)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10)
+    for it in range(10):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+        assert abs(stats[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
+        assert abs(stats[it].l1_delta - ref["l1"][it]) <= 1e-9 * max(ref["l1"][it], 1.0)
+
+
+def test_long_rows_and_unit_boundaries(hip, oracle_c):
+    """Hubs split into many 2048-in-link pieces, rows of exactly 2048 / 2049 in-links, and a
+    run of > 1024 short rows (the per-unit row cap)."""
+    rng = np.random.default_rng(9)
+    V = 30000
+    parts_s, parts_d = [], []
+    for hub, deg in [(0, 70000), (1, 2048), (2, 2049), (3, 4096), (4, 2047), (5, 1)]:
+        parts_s.append(rng.integers(0, V, deg))
+        parts_d.append(np.full(deg, hub))
+    parts_s.append(np.arange(V))
+    parts_d.append((np.arange(V) + 7) % V)
+    src = np.concatenate(parts_s).astype(np.int32)
+    dst = np.concatenate(parts_d).astype(np.int32)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 8)
+    assert info["n_long_rows"] >= 3
+    for it in range(8):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+
+
+def test_heavy_hub_and_many_indeg0(hip, oracle_c):
+    rng = np.random.default_rng(4)
+    src, dst = random_edges(rng, 20000, 300000, p_nolink=0.2, hub_frac=0.3)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 20000, src, dst, 10)
+    assert info["max_indeg"] > 50000
+    assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
+
+
+def test_dangling_none(hip, oracle_c):
+    rng = np.random.default_rng(5)
+    src, dst = random_edges(rng, 3000, 20000)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 3000, src, dst, 10, dangling="none")
+    assert all(s.dangling_sum == 0.0 for s in stats)
+    assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
+
+
+def test_resume_from_saved_ranks(hip, oracle_c):
+    rng = np.random.default_rng(6)
+    src, dst = random_edges(rng, 5000, 40000)
+    with hip.PageRankGraph(5000, src, dst) as g:
+        r5, _ = g.run(5)
+        r3, _ = g.run(3)
+        r3_2, _ = g.run(2, init_ranks=r3)
+    assert max_rel(r3_2, r5) <= 1e-13
+
+
+def test_deterministic_bitwise(hip):
+    rng = np.random.default_rng(7)
+    src, dst = random_edges(rng, 40000, 600000, hub_frac=0.05)
+    with hip.PageRankGraph(40000, src, dst) as g:
+        a, _ = g.run(10)
+        b, _ = g.run(10)
+    with hip.PageRankGraph(40000, src, dst) as g2:
+        c, _ = g2.run(10)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+
+
+def test_step_api_and_stats(hip, oracle_c):
+    rng = np.random.default_rng(8)
+    src, dst = random_edges(rng, 8000, 90000)
+    csr = oracle_c.build_csr(8000, src, dst)
+    ref = oracle_c.run(csr, 7)
+    with hip.PageRankGraph(8000, src, dst, keep_canonical=False) as g:
+        g.set_timing(True)
+        g.reset()
+        g.step(4)
+        g.step(3)
+        g.sync()
+        st = g.stats()
+        r = g.ranks()
+        with pytest.raises(hip.PageRankError):
+            g.export_csr()
+    assert st["iters"] == 7 and st["spmv_launches"] == 7 and st["spmv_ms_mean"] > 0
+    assert abs(st["last_dc"] - ref["dc"][6]) <= 1e-9 * ref["dc"][6]
+    assert abs(st["last_l1"] - ref["l1"][6]) <= 1e-9 * max(ref["l1"][6], 1)
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+
+
+def test_edge_cases(hip, oracle_c):
+    # empty graph
+    with hip.PageRankGraph(0, np.zeros(0, np.int32), np.zeros(0, np.int32)) as g:
+        r, st = g.run(3)
+        assert r.shape == (0,)
+    # only records without links: every vertex is a no-link key with in-degree 0 (keeps rank)
+    V = 5
+    with hip.PageRankGraph(V, np.arange(V, dtype=np.int32), np.full(V, -1, np.int32)) as g:
+        r, st = g.run(4)
+    csr = oracle_c.build_csr(V, np.arange(V, dtype=np.int32), np.full(V, -1, np.int32))
+    assert max_rel(r, oracle_c.run(csr, 4)["ranks"]) <= RANK_TOL
+    # malformed input fails loudly
+    with pytest.raises(hip.PageRankError) as e:
+        hip.PageRankGraph(3, np.array([0, 1], np.int32), np.array([1, 7], np.int32))
+    assert e.value.code == -1
+    with pytest.raises(hip.PageRankError):
+        hip.PageRankGraph(3, np.array([0], np.int32), np.array([1], np.int32))  # ID 2 never appears
+
+
+def host_first_appearance(src, dst):
+    occ = np.stack([src, dst], 1).ravel()
+    pos = np.arange(occ.size)
+    keep = occ >= 0
+    labels, first = np.unique(occ[keep], return_index=True)
+    order = np.argsort(pos[keep][first], kind="stable")
+    newid = np.full(labels.max() + 1 if labels.size else 1, -1, np.int64)
+    newid[labels[order]] = np.arange(labels.size)
+    s2 = newid[src]
+    d2 = np.where(dst >= 0, newid[np.maximum(dst, 0)], -1)
+    return labels.size, s2.astype(np.int32), d2.astype(np.int32)
+
+
+@pytest.mark.parametrize("gen,scale,ef", [("rmat", 14, 16), ("er", 13, 16), ("rmat", 18, 16)])
+def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef):
+    import torch
+
+    E = ef << scale
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    if gen == "rmat":
+        hip.gen_rmat(0, scale, E, s.data_ptr(), d.data_ptr(), seed=1)
+    else:
+        hip.gen_er(0, scale, E, s.data_ptr(), d.data_ptr(), seed=3)
+    torch.cuda.synchronize()
+    raw_s, raw_d = s.cpu().numpy(), d.cpu().numpy()
+    assert raw_s.min() >= 0 and raw_s.max() < (1 << scale)
+    V = hip.intern_device(0, E, 1 << scale, s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    Vh, hs, hd = host_first_appearance(raw_s, raw_d)
+    assert V == Vh
+    assert np.array_equal(s.cpu().numpy(), hs) and np.array_equal(d.cpu().numpy(), hd)
+    # graph from device-resident edges == graph from host edges == oracle
+    csr = oracle_c.build_csr(V, hs, hd)
+    ref = oracle_c.run(csr, 10)
+    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E) as g:
+        assert_csr_equal(g, csr)
+        r, st = g.run(10)
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+    # size-independent property: rank mass bookkeeping. Without no-link keys, the only
+    # change of sum(r) per iteration comes from in-degree-0 rows and the dangling term.
+    assert np.all(r >= 0.15)

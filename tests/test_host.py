@@ -1,0 +1,64 @@
+"""Host-side logic on CPU: tokeniser/interner, Java Double.toString, output writers."""
+import io
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+
+import sparky_rdd
+from sparky_hip import java_double_to_string, read_edge_list, write_has_rank, write_part_file
+
+
+@pytest.mark.parametrize("x,s", [
+    (1.1416666666666666, "1.1416666666666666"), (0.15, "0.15"), (1.0, "1.0"), (100.0, "100.0"),
+    (1e7, "1.0E7"), (9999999.0, "9999999.0"), (0.001, "0.001"), (9.99e-4, "9.99E-4"),
+    (12345678.9, "1.23456789E7"), (2e-5, "2.0E-5"), (1.2345e16, "1.2345E16"), (0.0, "0.0"),
+    (-0.0, "-0.0"), (-1.5, "-1.5"), (float("inf"), "Infinity"), (float("nan"), "NaN"),
+    (1e-300, "1.0E-300"), (123.456, "123.456"), (5e-324, "4.9E-324"),
+])
+def test_java_double_to_string(x, s):
+    assert java_double_to_string(x) == s
+
+
+def test_java_double_round_trips():
+    rng = random.Random(5)
+    for _ in range(2000):
+        x = struct.unpack("<d", struct.pack("<Q", rng.getrandbits(63)))[0]
+        if x != x or x in (float("inf"),):
+            continue
+        s = java_double_to_string(x)
+        assert float(s.replace("E", "e")) == x
+
+
+def test_reader_matches_oracle_interning(golden_cases):
+    for c in golden_cases:
+        urls, src, dst = read_edge_list(c["lines"])
+        names, osrc, odst = sparky_rdd.intern_first_appearance(sparky_rdd.pairs_from_edge_lines(c["lines"]))
+        assert urls == names == c["urls"]
+        assert src.tolist() == osrc and dst.tolist() == odst
+
+
+def test_reader_rejects_three_tokens():
+    with pytest.raises(ValueError):
+        read_edge_list(["a b c"])
+
+
+def test_reader_skips_blank_lines_and_keeps_tokens_verbatim():
+    urls, src, dst = read_edge_list(["", "http://a.b/?q=1 HTTP://A.B", "   ", "x"])
+    assert urls == ["http://a.b/?q=1", "HTTP://A.B", "x"]
+    assert src.tolist() == [0, 2] and dst.tolist() == [1, -1]
+
+
+def test_part_file_format(tmp_path):
+    d = write_part_file(str(tmp_path), 3, ["u1", "u2"], np.array([1.0, 0.7166666666666667]))
+    assert os.path.basename(d) == "PageRank3"
+    assert open(os.path.join(d, "part-00000")).read() == "(u1,1.0)\n(u2,0.7166666666666667)\n"
+    assert os.path.exists(os.path.join(d, "_SUCCESS"))
+
+
+def test_has_rank_format():
+    buf = io.StringIO()
+    write_has_rank(buf, ["a"], np.array([0.15]))
+    assert buf.getvalue() == "a has rank: 0.15.\n"
