@@ -62,3 +62,24 @@ def test_has_rank_format():
     buf = io.StringIO()
     write_has_rank(buf, ["a"], np.array([0.15]))
     assert buf.getvalue() == "a has rank: 0.15.\n"
+
+
+def test_cpp_formatter_matches_python():
+    """The C++ CLI's Double.toString (host/javafmt.h) == the Python host's, bit pattern by bit pattern."""
+    import subprocess
+
+    from conftest import PKG_DIR
+
+    exe = os.path.join(PKG_DIR, "build", "javafmt_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(PKG_DIR, "host"), exe], check=True)
+    rng = random.Random(11)
+    vals = [1.1416666666666666, 0.15, 1e7, 9999999.999999998, 1e-3, 9.99e-4, 5e-324, 2e-5, 1.0, 100.0,
+            123456.789, 1.7976931348623157e308, 0.0, -0.0, -2.5]
+    vals += [struct.unpack("<d", struct.pack("<Q", rng.getrandbits(63)))[0] for _ in range(3000)]
+    vals += [rng.uniform(0.15, 50.0) for _ in range(3000)]
+    vals = [v for v in vals if v == v]
+    inp = "".join(f"{struct.unpack('<Q', struct.pack('<d', v))[0]:x}\n" for v in vals)
+    out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split("\n")
+    for v, s in zip(vals, out):
+        assert s == java_double_to_string(v), (v, s)
