@@ -135,6 +135,15 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 int pr_comm_unique_id(uint8_t *id_out);
 int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8_t *id);
 
+/* Single process, one host thread, n_parts parts (one per GPU -- or several on one GPU): the
+ * parts exchange contributions by device-to-device copies (peer copies over xGMI between GPUs)
+ * instead of RCCL.  parts[p] must be part p of n_parts, created from the same edge list.
+ * Ranks: pr_get_ranks on every part (each fills its own vertices). */
+int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, double damping,
+                   const double *init_ranks);
+int pr_group_step(pr_graph *const *parts, int32_t n_parts, int32_t iterations);
+int pr_group_sync(pr_graph *const *parts, int32_t n_parts);
+
 void pr_graph_destroy(pr_graph *g);
 
 /* ---- synthetic inputs and device-side interning (benchmark front-end) ----------------- */

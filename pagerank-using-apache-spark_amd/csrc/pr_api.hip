@@ -318,12 +318,78 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
   return PR_OK;
 }
 
+static int check_group(pr_graph *const *parts, int32_t n) {
+  if (!parts || n < 1) return fail(PR_ERR_INVALID, "bad group");
+  for (int32_t p = 0; p < n; ++p) {
+    const pr_graph *g = parts[p];
+    if (!g) return fail(PR_ERR_INVALID, "NULL part in group");
+    if (g->nparts != n || g->part != p) return fail(PR_ERR_INVALID, "parts[p] must be part p of n_parts");
+    if (g->V != parts[0]->V || g->S_pad != parts[0]->S_pad) return fail(PR_ERR_INVALID, "parts of different graphs");
+    if (g->comm) return fail(PR_ERR_STATE, "a part with an RCCL communicator cannot join a group");
+  }
+  return PR_OK;
+}
+
+int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, double damping,
+                   const double *init_ranks) {
+  PR_TRY(check_group(parts, n_parts));
+  for (int32_t p = 0; p < n_parts; ++p) {
+    pr_graph *g = parts[p];
+    PR_HIP(hipSetDevice(g->device));
+    if (!g->xev) PR_HIP(hipEventCreateWithFlags(&g->xev, hipEventDisableTiming));
+    for (int32_t q = 0; q < n_parts; ++q) {  // peer access for xGMI copies between GPUs
+      if (parts[q]->device == g->device) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, g->device, parts[q]->device) == hipSuccess && can) {
+        hipError_t e = hipDeviceEnablePeerAccess(parts[q]->device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) PR_HIP(e);
+        (void)hipGetLastError();
+      }
+    }
+    g->grouped = true;
+    g->teleport = teleport;
+    g->damping = damping;
+    PR_TRY(pr::iter_reset(g, init_ranks));
+  }
+  PR_TRY(pr::group_exchange(parts, n_parts, 0));
+  for (int32_t p = 0; p < n_parts; ++p) {
+    PR_HIP(hipSetDevice(parts[p]->device));
+    PR_HIP(hipStreamSynchronize(parts[p]->stream));
+  }
+  return PR_OK;
+}
+
+int pr_group_step(pr_graph *const *parts, int32_t n_parts, int32_t iterations) {
+  PR_TRY(check_group(parts, n_parts));
+  if (iterations < 0) return fail(PR_ERR_INVALID, "iterations < 0");
+  for (int32_t p = 0; p < n_parts; ++p)
+    if (!parts[p]->grouped || !parts[p]->ready) return fail(PR_ERR_STATE, "pr_group_step before pr_group_reset");
+  for (int32_t it = 0; it < iterations; ++it) {
+    for (int32_t p = 0; p < n_parts; ++p) {
+      PR_HIP(hipSetDevice(parts[p]->device));
+      PR_TRY(pr::iter_compute(parts[p]));
+    }
+    PR_TRY(pr::group_exchange(parts, n_parts, parts[0]->cur));
+  }
+  return PR_OK;
+}
+
+int pr_group_sync(pr_graph *const *parts, int32_t n_parts) {
+  PR_TRY(check_group(parts, n_parts));
+  for (int32_t p = 0; p < n_parts; ++p) {
+    PR_HIP(hipSetDevice(parts[p]->device));
+    PR_HIP(hipStreamSynchronize(parts[p]->stream));
+  }
+  return PR_OK;
+}
+
 void pr_graph_destroy(pr_graph *g) {
   if (!g) return;
   DeviceGuard dg(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
+  if (g->xev) (void)hipEventDestroy(g->xev);
   g->ev_pool.clear();
   hipStream_t s = g->stream;
   g->stream = nullptr;

@@ -68,6 +68,9 @@ struct pr_graph {
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_size = 1;
+  // single-process group (pr_group_*): the group performs the exchange by device copies
+  bool grouped = false;
+  hipEvent_t xev = nullptr;
 
   size_t device_bytes() const;
 };
@@ -76,6 +79,8 @@ namespace pr {
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int iter_step(pr_graph *g, int32_t iterations);
+int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
+int group_exchange(pr_graph *const *parts, int n, int buf);
 int exchange(pr_graph *g, int buf);
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
 }  // namespace pr

@@ -333,7 +333,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
                      g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
   PR_HIP(hipGetLastError());
   PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0));
-  PR_TRY(exchange(g, 0));
+  if (!g->grouped) PR_TRY(exchange(g, 0));
   PR_HIP(hipStreamSynchronize(s));
   g->iters_done = 0;
   g->ready = true;
@@ -344,41 +344,81 @@ int iter_reset(pr_graph *g, const double *init_host) {
   return PR_OK;
 }
 
-int iter_step(pr_graph *g, int32_t iterations) {
-  if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
+int iter_compute(pr_graph *g) {
   hipStream_t s = g->stream;
   const int64_t own = (int64_t)g->part * g->S_pad;
+  const int in = g->cur, out = g->cur ^ 1;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (g->timing) {
+    e0 = next_event(g);
+    e1 = next_event(g);
+    if (!e0 || !e1) return fail(PR_ERR_HIP, "hipEventCreate failed");
+    PR_HIP(hipEventRecord(e0, s));
+  }
+  if (g->n_units > 0)
+    hipLaunchKernelGGL(k_spmv_units, dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
+                       g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->col.as<int32_t>(),
+                       g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
+                       g->degf.as<int32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
+                       g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping);
+  PR_HIP(hipGetLastError());
+  if (g->timing) {
+    PR_HIP(hipEventRecord(e1, s));
+    const int base = (int)g->ev_next - 2;
+    g->spmv_ev.push_back({base, base + 1});
+  }
+  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units, in, out));
+  g->cur = out;
+  ++g->iters_done;
+  return PR_OK;
+}
+
+int iter_step(pr_graph *g, int32_t iterations) {
+  if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
+  if (g->grouped) return fail(PR_ERR_STATE, "graph belongs to a group: use pr_group_step");
   for (int32_t it = 0; it < iterations; ++it) {
-    const int in = g->cur, out = g->cur ^ 1;
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, x0 = nullptr;
     if (g->timing) {
       e0 = next_event(g);
-      e1 = next_event(g);
-      e2 = next_event(g);
-      e3 = next_event(g);
-      if (!e0 || !e1 || !e2 || !e3) return fail(PR_ERR_HIP, "hipEventCreate failed");
-      PR_HIP(hipEventRecord(e0, s));
+      if (!e0) return fail(PR_ERR_HIP, "hipEventCreate failed");
+      PR_HIP(hipEventRecord(e0, g->stream));
     }
-    if (g->n_units > 0)
-      hipLaunchKernelGGL(k_spmv_units, dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
-                         g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->col.as<int32_t>(),
-                         g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
-                         g->degf.as<int32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
-                         g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping);
-    PR_HIP(hipGetLastError());
-    if (g->timing) PR_HIP(hipEventRecord(e1, s));
-    PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units, in, out));
-    if (g->timing) PR_HIP(hipEventRecord(e2, s));
-    PR_TRY(exchange(g, out));
+    const int i0 = (int)g->ev_next - 1;
+    PR_TRY(iter_compute(g));
     if (g->timing) {
-      PR_HIP(hipEventRecord(e3, s));
-      const int base = (int)g->ev_next - 4;
-      g->spmv_ev.push_back({base, base + 1});
-      g->xchg_ev.push_back({base + 2, base + 3});
-      g->iter_ev.push_back({base, base + 3});
+      x0 = next_event(g);
+      if (!x0) return fail(PR_ERR_HIP, "hipEventCreate failed");
+      PR_HIP(hipEventRecord(x0, g->stream));
     }
-    g->cur = out;
-    ++g->iters_done;
+    PR_TRY(exchange(g, g->cur));
+    if (g->timing) {
+      e1 = next_event(g);
+      if (!e1) return fail(PR_ERR_HIP, "hipEventCreate failed");
+      PR_HIP(hipEventRecord(e1, g->stream));
+      const int i1 = (int)g->ev_next - 1;
+      g->xchg_ev.push_back({i1 - 1, i1});
+      g->iter_ev.push_back({i0, i1});
+    }
+  }
+  return PR_OK;
+}
+
+// Single-process group: every part's slice (+ slots) is copied into every other part's gather
+// buffer after that part's finalize -- an all-gather by device copies (peer copies over xGMI
+// when the parts live on different GPUs).  Stream order: part p's copies wait on part q's event.
+int group_exchange(pr_graph *const *parts, int n, int buf) {
+  if (n <= 1) return PR_OK;
+  for (int q = 0; q < n; ++q) PR_HIP(hipEventRecord(parts[q]->xev, parts[q]->stream));
+  for (int p = 0; p < n; ++p) {
+    pr_graph *g = parts[p];
+    PR_HIP(hipSetDevice(g->device));
+    for (int q = 0; q < n; ++q) {
+      if (q == p) continue;
+      PR_HIP(hipStreamWaitEvent(g->stream, parts[q]->xev, 0));
+      const int64_t off = (int64_t)q * g->S_pad;
+      PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + off, parts[q]->cbuf[buf].as<double>() + off,
+                            sizeof(double) * g->S_pad, hipMemcpyDeviceToDevice, g->stream));
+    }
   }
   return PR_OK;
 }

@@ -5,11 +5,11 @@ reference job's I/O (edge list in, ``(url,rank)`` / ``<url> has rank: <r>.`` out
 """
 from ._lib import LIB_PATH, PageRankError, load
 from .driver import java_double_to_string, main, read_edge_list, write_has_rank, write_part_file
-from .graph import (CanonicalCSR, IterationStats, PageRankGraph, comm_unique_id, device_count, gen_er,
+from .graph import (CanonicalCSR, IterationStats, PageRankGraph, PartGroup, comm_unique_id, device_count, gen_er,
                     gen_rmat, intern_device)
 
 __all__ = [
     "LIB_PATH", "PageRankError", "load", "java_double_to_string", "main", "read_edge_list",
-    "write_has_rank", "write_part_file", "CanonicalCSR", "IterationStats", "PageRankGraph",
+    "write_has_rank", "write_part_file", "CanonicalCSR", "IterationStats", "PageRankGraph", "PartGroup",
     "comm_unique_id", "device_count", "gen_er", "gen_rmat", "intern_device",
 ]

@@ -40,7 +40,8 @@ EXPORTED = [
     "pr_abi_version", "pr_last_error", "pr_device_count", "pr_graph_create", "pr_graph_create_part",
     "pr_graph_info", "pr_graph_export_csr", "pr_run", "pr_reset", "pr_step", "pr_sync",
     "pr_get_ranks", "pr_set_timing", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
-    "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_intern_device",
+    "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_intern_device", "pr_group_reset",
+    "pr_group_step", "pr_group_sync",
 ]
 
 ITER_CB = ctypes.CFUNCTYPE(None, ctypes.c_int32, ctypes.POINTER(ctypes.c_double), ctypes.c_double,
@@ -90,6 +91,9 @@ def load() -> ctypes.CDLL:
         "pr_gen_rmat": ([i32, i32, i64, dbl, dbl, dbl, u64, P, P], ctypes.c_int),
         "pr_gen_er": ([i32, i32, i64, u64, P, P], ctypes.c_int),
         "pr_intern_device": ([i32, i64, i32, P, P, P], ctypes.c_int),
+        "pr_group_reset": ([P, i32, dbl, dbl, P], ctypes.c_int),
+        "pr_group_step": ([P, i32, i32], ctypes.c_int),
+        "pr_group_sync": ([P, i32], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

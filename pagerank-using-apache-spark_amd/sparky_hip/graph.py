@@ -196,3 +196,36 @@ def intern_device(device: int, n_edges: int, label_bound: int, src_ptr: int, dst
     check(_lib.load().pr_intern_device(device, n_edges, label_bound, ctypes.c_void_p(src_ptr),
                                        ctypes.c_void_p(dst_ptr), ctypes.byref(nv)))
     return nv.value
+
+
+class PartGroup:
+    """Single-process driver of several parts (pr_group_*): parts exchange contributions by
+    device copies (xGMI peer copies across GPUs).  The ranks of all parts are merged."""
+
+    def __init__(self, parts):
+        self.parts = list(parts)
+        n = len(self.parts)
+        self._arr = (ctypes.c_void_p * n)(*[p._h.value for p in self.parts])
+
+    def reset(self, *, teleport=0.15, damping=0.85, init_ranks=None):
+        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        check(_lib.load().pr_group_reset(self._arr, len(self.parts), teleport, damping, _ptr(init)))
+
+    def step(self, iterations: int):
+        check(_lib.load().pr_group_step(self._arr, len(self.parts), int(iterations)))
+
+    def sync(self):
+        check(_lib.load().pr_group_sync(self._arr, len(self.parts)))
+
+    def ranks(self) -> np.ndarray:
+        V = self.parts[0].n_vertices
+        out = np.full(max(V, 1), np.nan)
+        for p in self.parts:
+            p.ranks(out)
+        return out[:V]
+
+    def run(self, iterations: int, **kw) -> np.ndarray:
+        self.reset(**kw)
+        self.step(iterations)
+        self.sync()
+        return self.ranks()

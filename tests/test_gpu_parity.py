@@ -247,3 +247,29 @@ def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef):
     # size-independent property: rank mass bookkeeping. Without no-link keys, the only
     # change of sum(r) per iteration comes from in-degree-0 rows and the dangling term.
     assert np.all(r >= 0.15)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_row_partition_group_on_one_gpu(hip, oracle_c, P):
+    """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
+    exchange is the group's device-copy all-gather (RCCL carries it across processes)."""
+    rng = np.random.default_rng(30 + P)
+    V = 40000
+    src, dst = random_edges(rng, V, 500000, hub_frac=0.05)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 10)
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False) for p in range(P)]
+    try:
+        infos = [p.info() for p in parts]
+        assert sum(i["local_rows"] for i in infos) == V
+        assert sum(i["local_edges"] for i in infos) == csr.n_edges
+        grp = hip.PartGroup(parts)
+        r = grp.run(10)
+        assert not np.isnan(r).any()
+        assert max_rel(r, ref["ranks"]) <= RANK_TOL
+        # a part of a group refuses the single-part step
+        with pytest.raises(hip.PageRankError):
+            parts[0].step(1)
+    finally:
+        for p in parts:
+            p.close()
