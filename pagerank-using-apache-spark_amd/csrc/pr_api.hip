@@ -56,7 +56,7 @@ int exchange(pr_graph *g, int buf) {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + degf.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + degf.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes;
   return b;

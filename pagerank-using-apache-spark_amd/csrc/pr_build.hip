@@ -179,39 +179,70 @@ __global__ void k_local_rows(int64_t n_local, int P, int part, uint64_t mask, bo
 }  // namespace
 
 // Greedy work plan over the part's row_ptr (host; linear, deterministic).
-static void plan_units(const std::vector<int64_t> &rp, std::vector<Unit> &units,
-                       std::vector<int32_t> &lr_row, std::vector<int32_t> &lr_p0,
-                       int64_t *n_pieces) {
+void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan) {
   const int64_t R = (int64_t)rp.size() - 1;
-  int64_t pieces = 0;
-  int64_t v = 0;
-  units.clear();
-  lr_row.clear();
-  lr_p0.clear();
+  int64_t pieces = 0, pad = 0, v = 0;
+  plan->units.clear();
+  plan->src_off.clear();
+  plan->lr_row.clear();
+  plan->lr_p0.clear();
+  auto push = [&](int64_t src, int32_t r0, int32_t meta, int32_t n) {
+    plan->units.push_back(Unit{(uint32_t)(pad / 8), r0, meta, n});
+    plan->src_off.push_back(src);
+    pad += ((int64_t)n + 7) / 8 * 8;
+  };
   while (v < R) {
     const int64_t len = rp[v + 1] - rp[v];
-    if (len > kUnitNnz) {
-      const int64_t np = (len + kUnitNnz - 1) / kUnitNnz;
-      lr_row.push_back((int32_t)v);
-      lr_p0.push_back((int32_t)pieces);
-      for (int64_t q = 0; q < np; ++q)
-        units.push_back(Unit{rp[v] + q * kUnitNnz, (int32_t)v, (int32_t)(-(pieces + q) - 1)});
+    if (len > unit_nnz) {
+      const int64_t np = (len + unit_nnz - 1) / unit_nnz;
+      plan->lr_row.push_back((int32_t)v);
+      plan->lr_p0.push_back((int32_t)pieces);
+      for (int64_t q = 0; q < np; ++q) {
+        const int64_t n = std::min<int64_t>(unit_nnz, len - q * unit_nnz);
+        push(rp[v] + q * unit_nnz, (int32_t)v, (int32_t)(-(pieces + q) - 1), (int32_t)n);
+      }
       pieces += np;
       ++v;
       continue;
     }
     const int64_t start = v;
     int64_t nnz = 0;
-    while (v < R && v - start < kUnitRows) {
+    while (v < R && v - start < unit_rows) {
       const int64_t l = rp[v + 1] - rp[v];
-      if (l > kUnitNnz || nnz + l > kUnitNnz) break;
+      if (l > unit_nnz || nnz + l > unit_nnz) break;
       nnz += l;
       ++v;
     }
-    units.push_back(Unit{rp[start], (int32_t)start, (int32_t)(v - start)});
+    push(rp[start], (int32_t)start, (int32_t)(v - start), (int32_t)nnz);
   }
-  lr_p0.push_back((int32_t)pieces);
-  *n_pieces = pieces;
+  plan->lr_p0.push_back((int32_t)pieces);
+  plan->n_pieces = pieces;
+  plan->padded_len = pad;
+}
+
+namespace {
+__global__ void k_pad_cols(const Unit *__restrict__ units, const int64_t *__restrict__ src_off,
+                           const int32_t *__restrict__ col, int32_t *__restrict__ colp) {
+  const Unit u = units[blockIdx.x];
+  const int64_t s = src_off[blockIdx.x], d = (int64_t)u.p8 * 8;
+  for (int i = threadIdx.x; i < u.n; i += blockDim.x) colp[d + i] = col[s + i];
+}
+}  // namespace
+
+int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, hipStream_t s) {
+  const size_t nu = plan.units.size();
+  PR_HIP(hipMemsetAsync(colp, 0, sizeof(int32_t) * (plan.padded_len > 0 ? plan.padded_len : 1), s));
+  if (nu == 0) return PR_OK;
+  DevBuf du, ds;
+  PR_TRY(du.alloc(sizeof(Unit) * nu));
+  PR_TRY(ds.alloc(sizeof(int64_t) * nu));
+  PR_HIP(hipMemcpyAsync(du.p, plan.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
+  PR_HIP(hipMemcpyAsync(ds.p, plan.src_off.data(), sizeof(int64_t) * nu, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_pad_cols, dim3((unsigned)nu), dim3(256), 0, s, du.as<Unit>(), ds.as<int64_t>(),
+                     col, colp);
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipStreamSynchronize(s));
+  return PR_OK;
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
@@ -354,7 +385,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   rank_of.reset();
   gpos.reset();
 
-  // ---- work plan (host greedy over the part's row_ptr) ----
+  // ---- work plan (host greedy over the part's row_ptr) + padded gather-position array ----
   std::vector<int64_t> rp((size_t)g->n_local + 1);
   g->orig_of_local.resize((size_t)g->n_local);
   PR_HIP(hipMemcpyAsync(rp.data(), g->rowptr.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
@@ -362,21 +393,26 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * g->n_local,
                           hipMemcpyDeviceToHost, s));
   PR_HIP(hipStreamSynchronize(s));
-  std::vector<Unit> hu;
-  std::vector<int32_t> hlr, hp0;
-  plan_units(rp, hu, hlr, hp0, &g->n_pieces);
-  g->n_units = (int64_t)hu.size();
-  g->n_long = (int64_t)hlr.size();
-  PR_TRY(g->units.alloc(sizeof(Unit) * (hu.size() + 1)));
-  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * (hu.size() + 1)));
-  PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (hlr.size() + 1)));
-  PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (hp0.size() + 1)));
+  UnitPlan plan;
+  plan_units(rp, kUnitNnz, kUnitRows, &plan);
+  if (plan.padded_len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+  g->n_units = (int64_t)plan.units.size();
+  g->n_long = (int64_t)plan.lr_row.size();
+  g->n_pieces = plan.n_pieces;
+  PR_TRY(g->colp.alloc(sizeof(int32_t) * (plan.padded_len > 0 ? plan.padded_len : 8)));
+  PR_TRY(build_padded_cols(plan, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
+  g->col.reset();  // the unpadded copy is not needed by the iteration
+  PR_TRY(g->units.alloc(sizeof(Unit) * (plan.units.size() + 1)));
+  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * (plan.units.size() + 1)));
+  PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (plan.lr_row.size() + 1)));
+  PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (plan.lr_p0.size() + 1)));
   PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
-  if (!hu.empty())
-    PR_HIP(hipMemcpyAsync(g->units.p, hu.data(), sizeof(Unit) * hu.size(), hipMemcpyHostToDevice, s));
-  if (!hlr.empty())
-    PR_HIP(hipMemcpyAsync(g->lr_row.p, hlr.data(), sizeof(int32_t) * hlr.size(), hipMemcpyHostToDevice, s));
-  PR_HIP(hipMemcpyAsync(g->lr_p0.p, hp0.data(), sizeof(int32_t) * hp0.size(), hipMemcpyHostToDevice, s));
+  if (!plan.units.empty())
+    PR_HIP(hipMemcpyAsync(g->units.p, plan.units.data(), sizeof(Unit) * plan.units.size(), hipMemcpyHostToDevice, s));
+  if (!plan.lr_row.empty())
+    PR_HIP(hipMemcpyAsync(g->lr_row.p, plan.lr_row.data(), sizeof(int32_t) * plan.lr_row.size(), hipMemcpyHostToDevice, s));
+  PR_HIP(hipMemcpyAsync(g->lr_p0.p, plan.lr_p0.data(), sizeof(int32_t) * plan.lr_p0.size(), hipMemcpyHostToDevice, s));
+  PR_HIP(hipStreamSynchronize(s));
 
   // ---- iteration state ----
   PR_TRY(g->r.alloc(sizeof(double) * ((size_t)g->n_local + 1)));

@@ -69,4 +69,22 @@ __device__ __forceinline__ double block_sum(double x, double *scratch) {
   return t;
 }
 
+// Deterministic block sum of two doubles at once (one barrier pair).
+template <int NT>
+__device__ __forceinline__ double2 block_sum2(double2 x, double2 *scratch) {
+  constexpr int NW = NT / kWave;
+  x.x = wave_sum(x.x);
+  x.y = wave_sum(x.y);
+  if (lane_id() == 0) scratch[wave_id()] = x;
+  __syncthreads();
+  double2 t = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    t.x += scratch[w].x;
+    t.y += scratch[w].y;
+  }
+  __syncthreads();
+  return t;
+}
+
 }  // namespace pr

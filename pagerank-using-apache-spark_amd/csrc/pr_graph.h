@@ -9,7 +9,8 @@
 //                           positions in this space, so the RCCL all-gather of the slices is
 //                           the whole exchange (one call per iteration).
 //   rowptr  int64[n_local+1]  in-link CSR of the part's rows (local row order)
-//   col     int32[nnz]        gather positions, ascending within a row
+//   colp    int32[padded nnz]  gather positions, ascending within a row, grouped by work unit,
+//                             every unit 32-byte aligned (pr_spmv.h loads them as int4)
 //   degf    int32[n_local]    out-degree d>0; 0 = key without links; -1 = sink-only (in D)
 //   r       fp64[n_local]     ranks, updated in place
 //   cbuf    fp64[2][P*S_pad]  contributions r/d, double-buffered across iterations
@@ -43,7 +44,7 @@ struct pr_graph {
   bool has_canonical = false;
 
   // part layout
-  pr::DevBuf rowptr, col, degf, r;
+  pr::DevBuf rowptr, col, colp, degf, r;
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;

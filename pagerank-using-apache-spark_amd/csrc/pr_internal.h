@@ -73,18 +73,32 @@ inline unsigned grid_for(int64_t n, int threads, unsigned cap = 1u << 20) {
 
 // ---- SpMV work plan ------------------------------------------------------------------------
 // A unit is one workgroup of the SpMV launch.  STREAM: whole rows [r0, r0+meta) whose in-links
-// total <= kUnitNnz.  PIECE: kUnitNnz in-links of one long row r0 starting at e0; meta =
-// -(piece index + 1).
+// total n <= kUnitNnz.  PIECE: n <= kUnitNnz in-links of one long row r0; meta = -(piece+1).
+// Each unit's gather positions start at colp[8 * p8] (units padded to 32-byte boundaries).
 constexpr int kThreads = 256;       // workgroup size of the SpMV kernels (4 waves)
 constexpr int kPerThread = 8;       // in-links gathered per thread per unit
 constexpr int kUnitNnz = kThreads * kPerThread;  // 2048
 constexpr int kUnitRows = 1024;     // max rows per STREAM unit (LDS bound)
 
 struct Unit {
-  int64_t e0;
-  int32_t r0;
-  int32_t meta;
+  uint32_t p8;   // padded column offset / 8
+  int32_t r0;    // first row (STREAM) or the long row (PIECE)
+  int32_t meta;  // rows (>= 0) or -(piece index + 1)
+  int32_t n;     // in-links in the unit
 };
 static_assert(sizeof(Unit) == 16, "Unit must stay 16 bytes");
+
+// Host plan over a part's row_ptr: units, their source offsets in the unpadded column array,
+// long rows (split into pieces) and the padded column length.
+struct UnitPlan {
+  std::vector<Unit> units;
+  std::vector<int64_t> src_off;  // per unit: first in-link in the unpadded CSR
+  std::vector<int32_t> lr_row, lr_p0;
+  int64_t n_pieces = 0;
+  int64_t padded_len = 0;
+};
+void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan);
+// colp[8*p8 + i] = col[src_off + i] for every unit (padding entries are 0).
+int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, hipStream_t s);
 
 }  // namespace pr

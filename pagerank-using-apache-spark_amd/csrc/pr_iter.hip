@@ -26,181 +26,10 @@
 
 #include "pr_device.h"
 #include "pr_graph.h"
+#include "pr_spmv.h"
 
 namespace pr {
 namespace {
-
-__device__ __forceinline__ double dc_from_slots(const double *cin, int P, int64_t S_pad) {
-  double dc = 0.0;
-  for (int p = 0; p < P; ++p) dc = __dadd_rn(dc, cin[(int64_t)p * S_pad + S_pad - 2]);
-  return dc;
-}
-
-// r' = teleport + damping * (S + tdc), evaluated exactly as Sparky.java:233 (no contraction).
-__device__ __forceinline__ double affine(double S, double tdc, double teleport, double damping) {
-  return __dadd_rn(teleport, __dmul_rn(damping, __dadd_rn(S, tdc)));
-}
-
-__global__ __launch_bounds__(kThreads) void k_spmv_units(
-    const Unit *__restrict__ units, const int64_t *__restrict__ rowptr,
-    const int32_t *__restrict__ col, const double *__restrict__ cin, double *__restrict__ cout,
-    double *__restrict__ r, const int32_t *__restrict__ degf, double *__restrict__ piece_part,
-    double2 *__restrict__ unit_part, int P, int64_t S_pad, double n_vertices, double teleport,
-    double damping) {
-  __shared__ double val[kUnitNnz];
-  __shared__ double rowsum[kUnitRows];
-  __shared__ int32_t lrp[kUnitRows + 1];
-  __shared__ double red[kThreads / kWave];
-  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
-  __shared__ double wval_last[kThreads / kWave];
-
-  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const Unit u = units[blockIdx.x];
-
-  if (u.meta < 0) {  // ---- PIECE of a long row ----
-    const int64_t row_end = rowptr[u.r0 + 1];
-    int64_t n = row_end - u.e0;
-    if (n > kUnitNnz) n = kUnitNnz;
-    int32_t ci[kPerThread];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      const int i = j * kThreads + t;
-      ci[j] = (i < n) ? col[u.e0 + i] : -1;
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j)
-      if (ci[j] >= 0) acc = __dadd_rn(acc, cin[ci[j]]);
-    acc = block_sum<kThreads>(acc, red);
-    if (t == 0) {
-      piece_part[-u.meta - 1] = acc;
-      unit_part[blockIdx.x] = make_double2(0.0, 0.0);
-    }
-    return;
-  }
-
-  // ---- STREAM unit ----
-  const int nr = u.meta;
-  const int32_t r0 = u.r0;
-  const int64_t e0 = u.e0;
-  const int n = (int)(rowptr[r0 + nr] - e0);
-  for (int k = t; k <= nr; k += kThreads) lrp[k] = (int32_t)(rowptr[r0 + k] - e0);
-  {
-    int32_t ci[kPerThread];
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      const int i = j * kThreads + t;
-      ci[j] = (i < n) ? col[e0 + i] : -1;
-    }
-#pragma unroll
-    for (int j = 0; j < kPerThread; ++j) {
-      const int i = j * kThreads + t;
-      if (ci[j] >= 0) val[i] = cin[ci[j]];
-    }
-  }
-  const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
-  __syncthreads();
-
-  // Each thread reduces LDS elements [i0, i0+8) along row boundaries.
-  const int i0 = t * kPerThread;
-  int carry_row = -1, first_row = -1;
-  double carry_val = 0.0, first_sum = 0.0;
-  if (i0 < n) {
-    int lo = 0, hi = nr + 1;  // first k with lrp[k] > i0
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (lrp[mid] <= i0) lo = mid + 1;
-      else hi = mid;
-    }
-    int cur = lo - 1;
-    const int kstart = cur;
-    const bool started_before = lrp[cur] < i0;
-    int next_end = lrp[cur + 1];
-    const int iend = (i0 + kPerThread < n) ? i0 + kPerThread : n;
-    double acc = 0.0;
-    bool open = false;
-    for (int i = i0; i < iend; ++i) {
-      acc = __dadd_rn(acc, val[i]);
-      open = true;
-      if (i + 1 == next_end) {
-        if (cur == kstart && started_before) {
-          first_row = cur;
-          first_sum = acc;
-        } else {
-          rowsum[cur] = acc;
-        }
-        acc = 0.0;
-        open = false;
-        ++cur;
-        while (cur < nr && lrp[cur + 1] == lrp[cur]) ++cur;  // skip in-degree-0 rows
-        next_end = (cur < nr) ? lrp[cur + 1] : INT_MAX;
-      }
-    }
-    if (open) {
-      carry_row = cur;
-      carry_val = acc;
-    }
-  }
-
-  // Segmented inclusive scan of (carry_row, carry_val) over threads.  Equal rows are
-  // contiguous in thread order, so a Hillis-Steele step may add the partner's value when the
-  // partner carries the same row.
-  int srow = carry_row;
-  double sval = carry_val;
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const int prow = __shfl_up(srow, off, kWave);
-    const double pval = __shfl_up(sval, off, kWave);
-    if (lane >= off && srow >= 0 && prow == srow) sval = __dadd_rn(pval, sval);
-  }
-  const int lane0_row = __shfl(carry_row, 0, kWave);
-  if (lane == kWave - 1) {
-    wrow_last[w] = srow;
-    wval_last[w] = sval;
-    wrow_first[w] = lane0_row;
-  }
-  __syncthreads();
-  // carry-in from earlier waves (serial over <= 3 waves, identical in every lane)
-  int prow_in = -1;
-  double pval_in = 0.0;
-  for (int ww = 0; ww < w; ++ww) {
-    const int rl = wrow_last[ww];
-    const bool full = (rl >= 0) && (wrow_first[ww] == rl);
-    if (full && prow_in == rl) pval_in = __dadd_rn(pval_in, wval_last[ww]);
-    else {
-      prow_in = rl;
-      pval_in = (rl >= 0) ? wval_last[ww] : 0.0;
-    }
-  }
-  // extend this wave's leading segment with the carry-in
-  if (srow >= 0 && srow == prow_in && lane0_row == srow) sval = __dadd_rn(pval_in, sval);
-  // exclusive value seen by thread t = inclusive value of thread t-1
-  int erow = __shfl_up(srow, 1, kWave);
-  double eval = __shfl_up(sval, 1, kWave);
-  if (lane == 0) {
-    erow = prow_in;
-    eval = pval_in;
-  }
-  if (first_row >= 0) rowsum[first_row] = (erow == first_row) ? __dadd_rn(eval, first_sum) : first_sum;
-  __syncthreads();
-
-  // Epilogue over the unit's rows (coalesced).
-  double dcp = 0.0, l1p = 0.0;
-  for (int k = t; k < nr; k += kThreads) {
-    const int64_t v = (int64_t)r0 + k;
-    const double rold = r[v];
-    const double S = (lrp[k + 1] > lrp[k]) ? rowsum[k] : rold;
-    const double rn = affine(S, tdc, teleport, damping);
-    r[v] = rn;
-    const int32_t df = degf[v];
-    if (df > 0) cout[v] = __ddiv_rn(rn, (double)df);
-    else if (df < 0) dcp = __dadd_rn(dcp, rn);
-    l1p = __dadd_rn(l1p, fabs(rn - rold));
-  }
-  dcp = block_sum<kThreads>(dcp, red);
-  l1p = block_sum<kThreads>(l1p, red);
-  if (t == 0) unit_part[blockIdx.x] = make_double2(dcp, l1p);
-}
 
 __device__ __forceinline__ void store_sc1(double *p, double x) {
   __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), (unsigned long long)__double_as_longlong(x),
@@ -356,11 +185,11 @@ int iter_compute(pr_graph *g) {
     PR_HIP(hipEventRecord(e0, s));
   }
   if (g->n_units > 0)
-    hipLaunchKernelGGL(k_spmv_units, dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
-                       g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->col.as<int32_t>(),
+    hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
+                       g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
                        g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
                        g->degf.as<int32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
-                       g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping);
+                       g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
   PR_HIP(hipGetLastError());
   if (g->timing) {
     PR_HIP(hipEventRecord(e1, s));

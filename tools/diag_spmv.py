@@ -1,0 +1,71 @@
+"""A/B timing of SpMV kernel variants on one device-built graph (diagnostics, not product).
+
+usage: python tools/diag_spmv.py [--scale 26] [--rounds 3] [--iters 5] [--graph rmat|er]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=26)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--graph", default="rmat")
+    ap.add_argument("--variants", default="0,1,2,3,4:19,4:22,4:24")
+    a = ap.parse_args()
+    import torch
+
+    import sparky_hip
+
+    E = 16 << a.scale
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    if a.graph == "rmat":
+        sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=2)
+    else:
+        sparky_hip.gen_er(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=3)
+    V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E,
+                                 keep_canonical=False)
+    del s, d
+    torch.cuda.empty_cache()
+    info = g.info()
+    g.reset()
+    D = ctypes.CDLL(os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpagerank_diag.so"))
+    D.prd_time_spmv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_double)]
+    nbytes = 12 * info["local_edges"] + 36 * info["local_rows"]
+    print(f"graph {a.graph} s{a.scale}: V={V} E'={info['n_edges']} units={info['n_units']} "
+          f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
+    variants = []
+    for tok in a.variants.split(","):
+        if ":" in tok:
+            v, b = tok.split(":")
+            variants.append((int(v), (1 << int(b)) - 1, tok))
+        else:
+            variants.append((int(tok), 0xFFFFFFFF, tok))
+    res = {t: [] for _, _, t in variants}
+    for rnd in range(a.rounds):
+        for v, m, t in variants:
+            ms = ctypes.c_double()
+            rc = D.prd_time_spmv(g._h, v, m, a.iters, ctypes.byref(ms))
+            if rc != 0:
+                raise RuntimeError(f"variant {t}: rc={rc}")
+            res[t].append(ms.value)
+    for _, _, t in variants:
+        x = sorted(res[t])
+        med = x[len(x) // 2]
+        print(f"variant {t:>6}: median {med:8.3f} ms  min {x[0]:8.3f}  "
+              f"{nbytes / (med * 1e-3) / 1e9:8.1f} GB/s model  {info['n_edges'] / (med * 1e-3) / 1e9:7.1f} GTEPS",
+              flush=True)
+    g.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,4 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/r4_pytest.log 2>&1 && \
+timeout -k 10 300 python -u tools/diag_spmv.py --scale 26 --variants 0,1,2,3,4:6,4:12,4:19 > gpurun_out/r4_diag26.log 2>&1

@@ -41,6 +41,8 @@ def main():
     for r in stats:
         summary["kernels"].append({k: r[k] for k in r})
     spmv = [r for r in stats if KERNEL in r.get("Name", "")]
+    hit = counter_per_launch(os.path.join(d, "l2"), "TCC_HIT_sum")
+    miss = counter_per_launch(os.path.join(d, "l2"), "TCC_MISS_sum")
     fetch = counter_per_launch(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_per_launch(os.path.join(d, "write"), "WRITE_SIZE")
     res = {
@@ -51,6 +53,10 @@ def main():
         "fetch_size_kb_median": fetch[len(fetch) // 2] if fetch else None,
         "write_size_kb_median": write[len(write) // 2] if write else None,
     }
+    if hit and miss:
+        h, m = hit[len(hit) // 2], miss[len(miss) // 2]
+        res["l2_hit_rate"] = h / (h + m) if h + m > 0 else None
+        res["tcc_hit_median"], res["tcc_miss_median"] = h, m
     if fetch and write:
         res["hbm_bytes_per_launch"] = (2 * res["fetch_size_kb_median"] + res["write_size_kb_median"]) * 1024
         res["formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024, median over launches"
