@@ -167,3 +167,132 @@ def run(pairs, iterations: int = 10, dangling: str = "local", init: Optional[Dic
         history.append(ranks)
         dcs.append(dc)
     return g, history, dcs
+
+
+# ---- Common Crawl JSON front-end (Sparky.java:84-118), restated with Python's json -----------
+class _Num(str):
+    """A JSON number kept as its source text (Gson's LazilyParsedNumber prints it verbatim)."""
+
+
+def _reject_constant(name):
+    raise ValueError(f"non-JSON constant {name}")
+
+
+def _gson_str(s: str) -> str:
+    """JsonWriter.value(String) with htmlSafe = false (JsonElement.toString())."""
+    out = ['"']
+    for ch in s:
+        o = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif ch == "\t":
+            out.append("\\t")
+        elif ch == "\b":
+            out.append("\\b")
+        elif ch == "\n":
+            out.append("\\n")
+        elif ch == "\r":
+            out.append("\\r")
+        elif ch == "\f":
+            out.append("\\f")
+        elif o < 0x20:
+            out.append(f"\\u{o:04x}")
+        elif o in (0x2028, 0x2029):
+            out.append(f"\\u{o:04x}")
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def gson_to_string(v) -> str:
+    """JsonElement.toString() of a value parsed by _parse_json."""
+    if v is None:
+        return "null"
+    if v is True:
+        return "true"
+    if v is False:
+        return "false"
+    if isinstance(v, _Num):
+        return str.__str__(v)
+    if isinstance(v, str):
+        return _gson_str(v)
+    if isinstance(v, list):
+        return "[" + ",".join(gson_to_string(x) for x in v) + "]"
+    # object: list of (key, value) pairs; LinkedTreeMap keeps first position, last value
+    pairs = v[1]
+    last = {}
+    for k, x in pairs:
+        last[k] = x
+    seen, parts = set(), []
+    for k, _ in pairs:
+        if k in seen:
+            continue
+        seen.add(k)
+        parts.append(_gson_str(k) + ":" + gson_to_string(last[k]))
+    return "{" + ",".join(parts) + "}"
+
+
+def _parse_json(text: str):
+    import json
+
+    return json.loads(text, object_pairs_hook=lambda p: ("obj", p), parse_int=_Num,
+                      parse_float=_Num, parse_constant=_reject_constant)
+
+
+def _get(obj, key):
+    """JsonObject.get(name): last duplicate wins; None when absent."""
+    r = None
+    for k, x in obj[1]:
+        if k == key:
+            r = x
+    return r
+
+
+def _is_obj(v):
+    return isinstance(v, tuple) and len(v) == 2 and v[0] == "obj"
+
+
+def pairs_from_ccjson_lines(lines: Iterable[str]) -> List[Tuple[str, Optional[str]]]:
+    """'url<TAB>json' records -> the flatMapToPair output of Sparky.java:78-123.
+
+    Raises ValueError where the reference's executor would throw (malformed JSON,
+    ClassCastException / IllegalStateException on wrong types, NullPointerException on a link
+    without "href" or "type")."""
+    out: List[Tuple[str, Optional[str]]] = []
+    for ln, line in enumerate(lines):
+        line = line.rstrip("\n").rstrip("\r")
+        if not line:
+            continue
+        if "\t" not in line:
+            raise ValueError(f"line {ln + 1}: expected url<TAB>json")
+        url, text = line.split("\t", 1)
+        root = _parse_json(text)  # Sparky.java:87
+        if not _is_obj(root):  # :88
+            raise ValueError(f"line {ln + 1}: record is not a JSON object")
+        dangling = True  # :90
+        content = _get(root, "content")  # :89
+        if content is not None or any(k == "content" for k, _ in root[1]):
+            if not _is_obj(content):  # JsonNull / non-object -> ClassCastException
+                raise ValueError(f"line {ln + 1}: 'content' is not an object")
+            links = _get(content, "links")  # :93
+            if links is not None or any(k == "links" for k, _ in content[1]):
+                if not isinstance(links, list):
+                    raise ValueError(f"line {ln + 1}: 'links' is not an array")
+                for el in links:  # :98-110
+                    if not _is_obj(el):
+                        raise ValueError(f"line {ln + 1}: link is not an object")
+                    href, typ = _get(el, "href"), _get(el, "type")
+                    has_h = any(k == "href" for k, _ in el[1])
+                    has_t = any(k == "type" for k, _ in el[1])
+                    if not has_h or not has_t:
+                        raise ValueError(f"line {ln + 1}: link without href/type (NPE)")
+                    if gson_to_string(typ) != '"a"':  # :103
+                        continue
+                    out.append((url, gson_to_string(href).replace('"', "")))  # :101, :105, :107
+                    dangling = False
+        if dangling:
+            out.append((url, None))  # :114-118
+    return out

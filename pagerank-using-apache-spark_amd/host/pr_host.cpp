@@ -1,0 +1,560 @@
+// libpagerank_host: native input front-ends, URL interning and output writers (CPU).
+// See include/pagerank_host.h.  Everything before the GPU build and after the iteration.
+#include "pagerank_host.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <string>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+#include "javafmt.h"
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string &m) {
+  g_err = m;
+  return -1;
+}
+
+// ---- first-appearance interner over string_views (storage owned elsewhere) ----------------
+class Interner {
+ public:
+  explicit Interner(size_t expect) { rehash(expect < 1024 ? 2048 : next_pow2(expect * 2)); }
+  int32_t intern(std::string_view s) {
+    const uint64_t h = hash(s);
+    size_t i = h & mask_;
+    while (true) {
+      Slot &sl = slots_[i];
+      if (sl.id < 0) {
+        sl.id = (int32_t)names_.size();
+        sl.hash = h;
+        names_.push_back(s);
+        if (names_.size() * 2 > slots_.size()) rehash(slots_.size() * 2);
+        return (int32_t)names_.size() - 1;
+      }
+      if (sl.hash == h && names_[sl.id] == s) return sl.id;
+      i = (i + 1) & mask_;
+    }
+  }
+  std::vector<std::string_view> &names() { return names_; }
+
+ private:
+  struct Slot {
+    uint64_t hash;
+    int32_t id;
+  };
+  static size_t next_pow2(size_t x) {
+    size_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+  }
+  static uint64_t hash(std::string_view s) {  // FNV-1a 64 + murmur finaliser
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    return h ^ (h >> 33);
+  }
+  void rehash(size_t n) {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(n, Slot{0, -1});
+    mask_ = n - 1;
+    for (const Slot &sl : old) {
+      if (sl.id < 0) continue;
+      size_t i = sl.hash & mask_;
+      while (slots_[i].id >= 0) i = (i + 1) & mask_;
+      slots_[i] = sl;
+    }
+  }
+  std::vector<Slot> slots_;
+  std::vector<std::string_view> names_;
+  size_t mask_ = 0;
+};
+
+// ---- minimal JSON DOM (RFC 8259) with Gson JsonElement.toString() re-serialisation ----------
+struct JVal {
+  enum Kind { NUL, BOOL, NUM, STR, ARR, OBJ } kind = NUL;
+  bool b = false;
+  std::string s;  // NUM: source text; STR: decoded UTF-8
+  std::vector<JVal> arr;
+  std::vector<std::pair<std::string, JVal>> obj;  // insertion order, duplicate keys: last wins
+  const JVal *get(std::string_view k) const {
+    const JVal *r = nullptr;
+    for (auto &kv : obj)
+      if (kv.first == k) r = &kv.second;
+    return r;
+  }
+};
+
+class JParser {
+ public:
+  JParser(const char *p, const char *e) : p_(p), e_(e) {}
+  bool parse(JVal &out) {
+    if (!value(out, 0)) return false;
+    ws();
+    if (p_ != e_) return err("trailing characters");
+    return true;
+  }
+  std::string error;
+
+ private:
+  const char *p_, *e_;
+  bool err(const char *m) {
+    if (error.empty()) error = m;
+    return false;
+  }
+  void ws() {
+    while (p_ < e_ && (*p_ == ' ' || *p_ == '\t' || *p_ == '\n' || *p_ == '\r')) ++p_;
+  }
+  bool lit(const char *w) {
+    size_t n = std::strlen(w);
+    if ((size_t)(e_ - p_) < n || std::memcmp(p_, w, n) != 0) return err("bad literal");
+    p_ += n;
+    return true;
+  }
+  static void put_utf8(std::string &o, uint32_t cp) {
+    if (cp < 0x80) o.push_back((char)cp);
+    else if (cp < 0x800) { o.push_back((char)(0xC0 | (cp >> 6))); o.push_back((char)(0x80 | (cp & 0x3F))); }
+    else if (cp < 0x10000) {
+      o.push_back((char)(0xE0 | (cp >> 12)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    } else {
+      o.push_back((char)(0xF0 | (cp >> 18)));
+      o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+      o.push_back((char)(0x80 | (cp & 0x3F)));
+    }
+  }
+  bool hex4(uint32_t &v) {
+    if (e_ - p_ < 4) return err("short \\u escape");
+    v = 0;
+    for (int i = 0; i < 4; ++i) {
+      char c = *p_++;
+      v <<= 4;
+      if (c >= '0' && c <= '9') v |= (uint32_t)(c - '0');
+      else if (c >= 'a' && c <= 'f') v |= (uint32_t)(c - 'a' + 10);
+      else if (c >= 'A' && c <= 'F') v |= (uint32_t)(c - 'A' + 10);
+      else return err("bad \\u escape");
+    }
+    return true;
+  }
+  bool string(std::string &o) {
+    ++p_;  // opening quote
+    while (true) {
+      if (p_ >= e_) return err("unterminated string");
+      char c = *p_++;
+      if (c == '"') return true;
+      if ((unsigned char)c < 0x20) return err("control character in string");
+      if (c != '\\') { o.push_back(c); continue; }
+      if (p_ >= e_) return err("bad escape");
+      char x = *p_++;
+      switch (x) {
+        case '"': o.push_back('"'); break;
+        case '\\': o.push_back('\\'); break;
+        case '/': o.push_back('/'); break;
+        case 'b': o.push_back('\b'); break;
+        case 'f': o.push_back('\f'); break;
+        case 'n': o.push_back('\n'); break;
+        case 'r': o.push_back('\r'); break;
+        case 't': o.push_back('\t'); break;
+        case 'u': {
+          uint32_t v;
+          if (!hex4(v)) return false;
+          if (v >= 0xD800 && v < 0xDC00 && e_ - p_ >= 6 && p_[0] == '\\' && p_[1] == 'u') {
+            const char *save = p_;
+            p_ += 2;
+            uint32_t lo;
+            if (!hex4(lo)) return false;
+            if (lo >= 0xDC00 && lo < 0xE000) v = 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00);
+            else p_ = save;  // unpaired: keep as is
+          }
+          put_utf8(o, v);
+          break;
+        }
+        default: return err("bad escape");
+      }
+    }
+  }
+  bool number(JVal &o) {
+    const char *b = p_;
+    if (p_ < e_ && *p_ == '-') ++p_;
+    if (p_ >= e_ || !(*p_ >= '0' && *p_ <= '9')) return err("bad number");
+    while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' ||
+                       *p_ == '+' || *p_ == '-'))
+      ++p_;
+    o.kind = JVal::NUM;
+    o.s.assign(b, p_);
+    return true;
+  }
+  bool value(JVal &o, int depth) {
+    if (depth > 512) return err("nesting too deep");
+    ws();
+    if (p_ >= e_) return err("unexpected end");
+    char c = *p_;
+    if (c == '{') {
+      ++p_;
+      o.kind = JVal::OBJ;
+      ws();
+      if (p_ < e_ && *p_ == '}') { ++p_; return true; }
+      while (true) {
+        ws();
+        if (p_ >= e_ || *p_ != '"') return err("expected key");
+        std::string k;
+        if (!string(k)) return false;
+        ws();
+        if (p_ >= e_ || *p_ != ':') return err("expected ':'");
+        ++p_;
+        JVal v;
+        if (!value(v, depth + 1)) return false;
+        o.obj.emplace_back(std::move(k), std::move(v));
+        ws();
+        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (p_ < e_ && *p_ == '}') { ++p_; return true; }
+        return err("expected ',' or '}'");
+      }
+    }
+    if (c == '[') {
+      ++p_;
+      o.kind = JVal::ARR;
+      ws();
+      if (p_ < e_ && *p_ == ']') { ++p_; return true; }
+      while (true) {
+        JVal v;
+        if (!value(v, depth + 1)) return false;
+        o.arr.push_back(std::move(v));
+        ws();
+        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (p_ < e_ && *p_ == ']') { ++p_; return true; }
+        return err("expected ',' or ']'");
+      }
+    }
+    if (c == '"') {
+      o.kind = JVal::STR;
+      return string(o.s);
+    }
+    if (c == 't') { o.kind = JVal::BOOL; o.b = true; return lit("true"); }
+    if (c == 'f') { o.kind = JVal::BOOL; o.b = false; return lit("false"); }
+    if (c == 'n') { o.kind = JVal::NUL; return lit("null"); }
+    return number(o);
+  }
+};
+
+// Gson JsonWriter string escaping (htmlSafe = false, the JsonElement.toString() writer).
+void gson_string(std::string &o, const std::string &s) {
+  static const char *hex = "0123456789abcdef";
+  o.push_back('"');
+  for (size_t i = 0; i < s.size(); ++i) {
+    unsigned char c = (unsigned char)s[i];
+    switch (c) {
+      case '"': o += "\\\""; continue;
+      case '\\': o += "\\\\"; continue;
+      case '\t': o += "\\t"; continue;
+      case '\b': o += "\\b"; continue;
+      case '\n': o += "\\n"; continue;
+      case '\r': o += "\\r"; continue;
+      case '\f': o += "\\f"; continue;
+      default: break;
+    }
+    if (c < 0x20) {
+      o += "\\u00";
+      o.push_back(hex[c >> 4]);
+      o.push_back(hex[c & 15]);
+      continue;
+    }
+    // U+2028 / U+2029 (E2 80 A8 / E2 80 A9 in UTF-8)
+    if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+        ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+      o += ((unsigned char)s[i + 2] == 0xA8) ? "\\u2028" : "\\u2029";
+      i += 2;
+      continue;
+    }
+    o.push_back((char)c);
+  }
+  o.push_back('"');
+}
+
+void gson_to_string(std::string &o, const JVal &v) {
+  switch (v.kind) {
+    case JVal::NUL: o += "null"; break;
+    case JVal::BOOL: o += v.b ? "true" : "false"; break;
+    case JVal::NUM: o += v.s; break;
+    case JVal::STR: gson_string(o, v.s); break;
+    case JVal::ARR:
+      o.push_back('[');
+      for (size_t i = 0; i < v.arr.size(); ++i) {
+        if (i) o.push_back(',');
+        gson_to_string(o, v.arr[i]);
+      }
+      o.push_back(']');
+      break;
+    case JVal::OBJ: {
+      // LinkedTreeMap: a repeated key keeps its first position and its last value
+      o.push_back('{');
+      bool first = true;
+      for (size_t i = 0; i < v.obj.size(); ++i) {
+        bool seen = false;
+        for (size_t j = 0; j < i; ++j)
+          if (v.obj[j].first == v.obj[i].first) seen = true;
+        if (seen) continue;
+        if (!first) o.push_back(',');
+        first = false;
+        gson_string(o, v.obj[i].first);
+        o.push_back(':');
+        gson_to_string(o, *v.get(v.obj[i].first));
+      }
+      o.push_back('}');
+      break;
+    }
+  }
+}
+
+}  // namespace
+
+struct prh_edges {
+  std::shared_ptr<void> mapping;     // mmap'd file or copied buffer backing the name views
+  std::deque<std::string> arena;     // names created by the JSON front-end
+  std::vector<std::string_view> names;
+  std::vector<int32_t> src, dst;
+};
+
+namespace {
+
+struct Mapping {
+  void *p = nullptr;
+  size_t n = 0;
+  ~Mapping() {
+    if (p && n) munmap(p, n);
+  }
+};
+
+// Sparky.java:84-118 for one record: (url, href) per type=="a" link, or (url, null).
+int extract_links(std::string_view url, const char *jb, const char *je, prh_edges *E, Interner &in,
+                  size_t lineno) {
+  JVal root;
+  JParser jp(jb, je);
+  if (!jp.parse(root))
+    return fail("line " + std::to_string(lineno) + ": JSON: " + jp.error);
+  if (root.kind != JVal::OBJ)  // getAsJsonObject() on a non-object (Sparky.java:88)
+    return fail("line " + std::to_string(lineno) + ": record is not a JSON object");
+  const int32_t su = in.intern(url);
+  bool dangling = true;  // Sparky.java:90
+  const JVal *content = root.get("content");  // :89
+  if (content) {
+    if (content->kind != JVal::OBJ)
+      return fail("line " + std::to_string(lineno) + ": 'content' is not an object (ClassCastException in the reference)");
+    const JVal *links = content->get("links");  // :93
+    if (links) {
+      if (links->kind != JVal::ARR)
+        return fail("line " + std::to_string(lineno) + ": 'links' is not an array");
+      for (const JVal &el : links->arr) {  // :98
+        if (el.kind != JVal::OBJ)
+          return fail("line " + std::to_string(lineno) + ": link is not an object");
+        const JVal *href = el.get("href"), *type = el.get("type");
+        if (!href || !type)  // temp.get(...).toString() on null: NPE (:101-102)
+          return fail("line " + std::to_string(lineno) + ": link without 'href' or 'type' (NullPointerException in the reference)");
+        std::string ts;
+        gson_to_string(ts, *type);
+        if (ts != "\"a\"") continue;  // :103
+        std::string hs;
+        gson_to_string(hs, *href);  // :101
+        std::string stripped;
+        stripped.reserve(hs.size());
+        for (char ch : hs)
+          if (ch != '"') stripped.push_back(ch);  // aLink.replace("\"", "") (:105)
+        dangling = false;
+        E->arena.push_back(std::move(stripped));
+        E->src.push_back(su);
+        E->dst.push_back(in.intern(E->arena.back()));
+      }
+    }
+  }
+  if (dangling) {  // (url, null) (:114-118)
+    E->src.push_back(su);
+    E->dst.push_back(-1);
+  }
+  return 0;
+}
+
+int parse_into(const char *data, size_t n, int32_t format, prh_edges *E) {
+  Interner in(n / 32);
+  size_t i = 0, lineno = 0;
+  while (i < n) {
+    ++lineno;
+    size_t b = i;
+    while (i < n && data[i] != '\n') ++i;
+    size_t e = i;
+    ++i;
+    if (e > b && data[e - 1] == '\r') --e;
+    if (format == PRH_FORMAT_CCJSON) {
+      if (e == b) continue;
+      const char *tab = static_cast<const char *>(std::memchr(data + b, '\t', e - b));
+      if (!tab) return fail("line " + std::to_string(lineno) + ": expected 'url<TAB>json'");
+      if (extract_links(std::string_view(data + b, (size_t)(tab - (data + b))), tab + 1, data + e, E, in,
+                        lineno) != 0)
+        return -1;
+      continue;
+    }
+    std::string_view tok[3];
+    int nt = 0;
+    size_t j = b;
+    while (j < e) {
+      while (j < e && (data[j] == ' ' || data[j] == '\t')) ++j;
+      if (j >= e) break;
+      size_t tb = j;
+      while (j < e && data[j] != ' ' && data[j] != '\t') ++j;
+      if (nt < 3) tok[nt] = std::string_view(data + tb, j - tb);
+      ++nt;
+    }
+    if (nt == 0) continue;
+    if (nt > 2)
+      return fail("line " + std::to_string(lineno) + ": expected 'src [dst]', got " + std::to_string(nt) + " tokens");
+    E->src.push_back(in.intern(tok[0]));
+    E->dst.push_back(nt == 2 ? in.intern(tok[1]) : -1);
+  }
+  E->names.swap(in.names());
+  if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
+  return 0;
+}
+
+bool mkdirs(const std::string &p) {
+  std::string cur;
+  for (size_t i = 0; i <= p.size(); ++i) {
+    if (i == p.size() || p[i] == '/') {
+      if (!cur.empty() && mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+    if (i < p.size()) cur.push_back(p[i]);
+  }
+  return true;
+}
+
+template <class Line>
+int write_lines(FILE *f, const prh_edges *e, const double *ranks, Line line) {
+  std::string buf;
+  buf.reserve(1 << 20);
+  for (size_t v = 0; v < e->names.size(); ++v) {
+    line(buf, e->names[v], ranks[v]);
+    if (buf.size() > (1 << 20) - 8192) {
+      if (std::fwrite(buf.data(), 1, buf.size(), f) != buf.size()) return fail("write failed");
+      buf.clear();
+    }
+  }
+  if (std::fwrite(buf.data(), 1, buf.size(), f) != buf.size()) return fail("write failed");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *prh_last_error(void) { return g_err.c_str(); }
+
+int prh_read(const char *path, int32_t format, prh_edges **out) {
+  if (!path || !out) return fail("NULL argument");
+  if (format != PRH_FORMAT_EDGES && format != PRH_FORMAT_CCJSON) return fail("unknown format");
+  *out = nullptr;
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(std::string("cannot open ") + path + ": " + std::strerror(errno));
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return fail("fstat failed");
+  }
+  auto m = std::make_shared<Mapping>();
+  m->n = (size_t)st.st_size;
+  if (m->n > 0) {
+    m->p = mmap(nullptr, m->n, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m->p == MAP_FAILED) {
+      m->p = nullptr;
+      close(fd);
+      return fail("mmap failed");
+    }
+    madvise(m->p, m->n, MADV_SEQUENTIAL);
+  }
+  close(fd);
+  std::unique_ptr<prh_edges> e(new prh_edges());
+  e->mapping = m;
+  if (parse_into(static_cast<const char *>(m->p ? m->p : (void *)""), m->n, format, e.get()) != 0) return -1;
+  *out = e.release();
+  return 0;
+}
+
+int prh_parse(const char *data, int64_t len, int32_t format, prh_edges **out) {
+  if ((!data && len > 0) || !out || len < 0) return fail("bad argument");
+  if (format != PRH_FORMAT_EDGES && format != PRH_FORMAT_CCJSON) return fail("unknown format");
+  *out = nullptr;
+  auto buf = std::make_shared<std::string>(data ? std::string(data, (size_t)len) : std::string());
+  std::unique_ptr<prh_edges> e(new prh_edges());
+  e->mapping = buf;
+  if (parse_into(buf->data(), buf->size(), format, e.get()) != 0) return -1;
+  *out = e.release();
+  return 0;
+}
+
+int64_t prh_n_edges(const prh_edges *e) { return e ? (int64_t)e->src.size() : -1; }
+int32_t prh_n_vertices(const prh_edges *e) { return e ? (int32_t)e->names.size() : -1; }
+const int32_t *prh_src(const prh_edges *e) { return e ? e->src.data() : nullptr; }
+const int32_t *prh_dst(const prh_edges *e) { return e ? e->dst.data() : nullptr; }
+
+const char *prh_name(const prh_edges *e, int32_t id, int64_t *len) {
+  if (!e || id < 0 || (size_t)id >= e->names.size()) return nullptr;
+  if (len) *len = (int64_t)e->names[id].size();
+  return e->names[id].data();
+}
+
+int32_t prh_java_double(double x, char *buf) { return (int32_t)pr_host::java_double_to_string(x, buf); }
+
+int prh_write_part(const prh_edges *e, const char *dir, int32_t iter, const double *ranks) {
+  if (!e || !dir || !ranks) return fail("NULL argument");
+  const std::string d = std::string(dir) + "/PageRank" + std::to_string(iter);
+  if (!mkdirs(d)) return fail("cannot create " + d);
+  FILE *f = std::fopen((d + "/part-00000").c_str(), "w");
+  if (!f) return fail("cannot write " + d + "/part-00000");
+  char num[64];
+  int rc = write_lines(f, e, ranks, [&](std::string &b, std::string_view u, double r) {
+    b.push_back('(');
+    b.append(u);
+    b.push_back(',');
+    b.append(num, pr_host::java_double_to_string(r, num));
+    b.append(")\n");
+  });
+  std::fclose(f);
+  if (rc) return rc;
+  FILE *s = std::fopen((d + "/_SUCCESS").c_str(), "w");
+  if (!s) return fail("cannot write _SUCCESS");
+  std::fclose(s);
+  return 0;
+}
+
+int prh_write_has_rank(const prh_edges *e, const char *path, const double *ranks) {
+  if (!e || !ranks) return fail("NULL argument");
+  FILE *f = path ? std::fopen(path, "w") : stdout;
+  if (!f) return fail(std::string("cannot write ") + path);
+  char num[64];
+  int rc = write_lines(f, e, ranks, [&](std::string &b, std::string_view u, double r) {
+    b.append(u);
+    b.append(" has rank: ");
+    b.append(num, pr_host::java_double_to_string(r, num));
+    b.append(".\n");
+  });
+  if (path) std::fclose(f);
+  else std::fflush(f);
+  return rc;
+}
+
+void prh_free(prh_edges *e) { delete e; }
+
+}  // extern "C"

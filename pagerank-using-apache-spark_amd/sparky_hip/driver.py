@@ -1,7 +1,7 @@
 """Process-level drop-in for the Spark job (Python host; the C++ CLI ``pagerank`` is the same).
 
-CLI: ``python -m sparky_hip <edge-list-path> [iterations=10] [--out DIR]
-[--save-every-iter] [--dangling=local|none] [--device N] [--quiet]``
+CLI: ``python -m sparky_hip <input-path> [iterations=10] [--format edges|ccjson]
+[--out DIR] [--save-every-iter] [--dangling=local|none] [--device N] [--quiet]``
 
 * input: text edge list, ``src dst`` per line; a single-token line ``src`` is a record without
   ``a`` links (Sparky.java:114-118).  Tokens (URLs) are taken verbatim and interned to dense
@@ -122,36 +122,35 @@ def write_has_rank(stream: TextIO, urls: Sequence[str], ranks: np.ndarray) -> No
 
 
 def main(argv=None) -> int:
+    from ._host import HostEdges
+
     ap = argparse.ArgumentParser(prog="sparky_hip", description=__doc__.splitlines()[0])
     ap.add_argument("edge_list")
     ap.add_argument("iterations", nargs="?", type=int, default=10)  # Sparky.java:187
+    ap.add_argument("--format", choices=["edges", "ccjson"], default="edges")
     ap.add_argument("--out", default=None)
     ap.add_argument("--save-every-iter", action="store_true")
     ap.add_argument("--dangling", choices=["local", "none"], default="local")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--quiet", action="store_true", help="omit the '<url> has rank' lines")
     a = ap.parse_args(argv)
-    with open(a.edge_list) as f:
-        urls, src, dst = read_edge_list(f)
+    edges = HostEdges.read(a.edge_list, a.format)  # native front-end + first-appearance interning
     out = sys.stdout
-    with PageRankGraph(len(urls), src, dst, device=a.device, dangling=a.dangling,
+    with PageRankGraph(edges.n_vertices, edges.src, edges.dst, device=a.device, dangling=a.dangling,
                        keep_canonical=False) as g:
-        def cb(it, ranks, _st):
-            if a.out and (a.save_every_iter or it == a.iterations - 1):
-                write_part_file(a.out, it, urls, ranks)
-
         # Sparky prints "Starting iter<i>" before each iteration (Sparky.java:188); the library
         # calls back after iteration i, so the host prints the next line there.
-        def cb_print(it, ranks, st):
-            cb(it, ranks, st)
+        def cb(it, ranks, _st):
+            if a.out and (a.save_every_iter or it == a.iterations - 1):
+                edges.write_part(a.out, it, ranks)
             if it + 1 < a.iterations:
                 out.write(f"Starting iter{it + 1}\n")
 
         if a.iterations > 0:
             out.write("Starting iter0\n")
-        ranks, _ = g.run(a.iterations, callback=cb_print,
-                         want_ranks_in_callback=bool(a.out))
-    if not a.quiet:
-        write_has_rank(out, urls, ranks)
+        ranks, _ = g.run(a.iterations, callback=cb, want_ranks_in_callback=bool(a.out))
     out.flush()
+    if not a.quiet:
+        edges.write_has_rank(None, ranks)
+    edges.close()
     return 0

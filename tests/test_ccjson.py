@@ -1,0 +1,109 @@
+"""Common Crawl JSON front-end (Sparky.java:78-123) on CPU: the native
+libpagerank_host parser against the oracle restatement (oracle/sparky_rdd.py), including the
+Gson JsonElement.toString() quirks the reference's `aLink.replace("\"", "")` relies on."""
+import json
+import random
+
+import pytest
+
+import sparky_rdd
+from sparky_hip import HostEdges, HostError
+
+RECORDS = [
+    ("http://a.com/", {"content": {"links": [{"href": "http://b.com/", "type": "a"},
+                                             {"href": "http://c.com/", "type": "link"},
+                                             {"href": "http://b.com/", "type": "a"}]}}),
+    ("http://b.com/", {"content": {"links": []}}),  # empty links: dangling record
+    ("http://c.com/", {"content": {}}),  # no links
+    ("http://d.com/", {"other": 1}),  # no content
+    ("http://e.com/", {"content": {"links": [{"href": "q\"uote\\back", "type": "a"}]}}),
+    ("http://f.com/", {"content": {"links": [{"href": "tab\there\nnl\u0001ctl ls", "type": "a"}]}}),
+    ("http://g.com/", {"content": {"links": [{"href": "üñí©ødé/路径", "type": "a"}]}}),
+    ("http://h.com/", {"content": {"links": [{"href": 12.50, "type": "a"}, {"href": True, "type": "a"},
+                                             {"href": None, "type": "a"},
+                                             {"href": {"k": "v", "n": [1, "x"]}, "type": "a"}]}}),
+    ("http://i.com/", {"content": {"links": [{"href": "http://a.com/", "type": "A"},
+                                             {"href": "http://a.com/", "type": ["a"]}]}}),
+    ("http://j.com/", {"content": {"links": [{"href": "http://j.com/", "type": "a"}]}}),  # self loop
+]
+
+
+def lines():
+    return [f"{u}\t{json.dumps(j, ensure_ascii=False)}" for u, j in RECORDS]
+
+
+def native(text: str, fmt="ccjson"):
+    e = HostEdges.parse(text.encode("utf-8"), fmt)
+    names = e.names()
+    out = [(names[s], None if d < 0 else names[d]) for s, d in zip(e.src.tolist(), e.dst.tolist())]
+    e.close()
+    return out, names
+
+
+def test_ccjson_matches_oracle():
+    want = sparky_rdd.pairs_from_ccjson_lines(lines())
+    got, names = native("\n".join(lines()) + "\n")
+    assert got == want
+    wnames, _, _ = sparky_rdd.intern_first_appearance(want)
+    assert names == wnames
+    d = dict((u, v) for u, v in want if u == "http://e.com/")
+    assert d["http://e.com/"] == "q\\uote\\\\back"  # escaped quote keeps its backslash
+    hrefs = [v for u, v in want if u == "http://h.com/"]
+    assert hrefs == ["12.5", "true", "null", "{k:v,n:[1,x]}"]  # numbers keep their source text
+    assert ("http://i.com/", None) in want  # "A" / ["a"] are not type "a"
+
+
+def test_ccjson_number_source_text_kept():
+    text = 'u\t{"content":{"links":[{"href":1.50e+2,"type":"a"}]}}'
+    assert native(text)[0] == sparky_rdd.pairs_from_ccjson_lines([text]) == [("u", "1.50e+2")]
+
+
+def test_ccjson_duplicate_keys_last_wins():
+    text = 'u\t{"content":{"links":[{"href":"x","type":"a","href":"y"}]}}'
+    want = sparky_rdd.pairs_from_ccjson_lines([text])
+    got, _ = native(text)
+    assert got == want == [("u", "y")]
+
+
+@pytest.mark.parametrize("bad", [
+    'u\t[1,2]',  # not an object (IllegalStateException)
+    'u\t{"content":[1]}',  # content not an object
+    'u\t{"content":null}',  # JsonNull -> ClassCastException
+    'u\t{"content":{"links":{"a":1}}}',  # links not an array
+    'u\t{"content":{"links":[{"type":"a"}]}}',  # missing href -> NPE
+    'u\t{"content":{"links":[{"href":"x"}]}}',  # missing type -> NPE
+    'u\t{"content":{"links":[3]}}',  # link not an object
+    'u\t{"content": {',  # malformed JSON
+    'no tab here',
+])
+def test_ccjson_errors_like_reference(bad):
+    with pytest.raises(ValueError):
+        sparky_rdd.pairs_from_ccjson_lines([bad])
+    with pytest.raises(HostError):
+        native(bad)
+
+
+def test_ccjson_random_records():
+    rng = random.Random(3)
+    alphabet = ["a", "b", "/", "\"", "\\", "\t", "é", " ", " ", "?", "="]
+    recs = []
+    for i in range(300):
+        links = []
+        for _ in range(rng.randrange(0, 6)):
+            href = "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 8)))
+            links.append({"href": href, "type": rng.choice(["a", "a", "img", "link"])})
+        rec = {"content": {"links": links}} if rng.random() < 0.9 else {}
+        recs.append(f"u{rng.randrange(100)}\t{json.dumps(rec, ensure_ascii=rng.random() < 0.5)}")
+    want = sparky_rdd.pairs_from_ccjson_lines(recs)
+    got, _ = native("\n".join(recs))
+    assert got == want
+
+
+def test_native_edge_list_matches_python_reader(golden_cases):
+    import sparky_hip
+
+    for c in golden_cases:
+        got, names = native("\n".join(c["lines"]) + "\n", "edges")
+        urls, src, dst = sparky_hip.read_edge_list(c["lines"])
+        assert names == urls
+        assert got == [(urls[s], None if d < 0 else urls[d]) for s, d in zip(src.tolist(), dst.tolist())]

@@ -1,0 +1,91 @@
+"""End-to-end drop-in on the GPU: the C++ `pagerank` CLI and `python -m sparky_hip` on edge-list
+and Common Crawl JSON inputs; stdout lines and (url,rank) part files against the oracle."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import sparky_rdd
+from conftest import PKG_DIR
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(PKG_DIR, "build", "pagerank")
+KAT = ["A B", "A C", "A B", "B C", "C A", "C C", "D", "E A", "E F"]
+
+
+def parse_has_rank(text):
+    out = {}
+    for line in text.splitlines():
+        if " has rank: " in line:
+            u, r = line.rsplit(" has rank: ", 1)
+            assert r.endswith(".")
+            out[u] = float(r[:-1])
+    return out
+
+
+def parse_part(path):
+    out = {}
+    for line in open(path):
+        assert line.startswith("(") and line.endswith(")\n")
+        u, r = line[1:-2].rsplit(",", 1)
+        out[u] = float(r)
+    return out
+
+
+def oracle(pairs, iters):
+    g, hist, _ = sparky_rdd.run(pairs, iters)
+    return hist
+
+
+@pytest.mark.parametrize("runner", ["cpp", "python"])
+def test_cli_edge_list(tmp_path, runner):
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(KAT) + "\n")
+    out_dir = tmp_path / "out"
+    if runner == "cpp":
+        cmd = [CLI, str(inp), "3", "--out", str(out_dir), "--save-every-iter"]
+    else:
+        cmd = [sys.executable, "-m", "sparky_hip", str(inp), "3", "--out", str(out_dir), "--save-every-iter"]
+    env = dict(os.environ, PYTHONPATH=PKG_DIR)
+    res = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr
+    lines = res.stdout.splitlines()
+    assert lines[:3] == ["Starting iter0", "Starting iter1", "Starting iter2"]
+    hist = oracle(sparky_rdd.pairs_from_edge_lines(KAT), 3)
+    got = parse_has_rank(res.stdout)
+    assert got.keys() == hist[-1].keys()
+    for u, v in hist[-1].items():
+        assert abs(got[u] - v) <= 1e-9 * v
+    for it in range(3):
+        part = parse_part(out_dir / f"PageRank{it}" / "part-00000")
+        assert (out_dir / f"PageRank{it}" / "_SUCCESS").exists()
+        for u, v in hist[it].items():
+            assert abs(part[u] - v) <= 1e-9 * v
+
+
+def test_cli_ccjson(tmp_path):
+    rng = np.random.default_rng(2)
+    recs = []
+    for i in range(400):
+        links = [{"href": f"http://s{int(rng.integers(0, 300))}.org/", "type": "a" if rng.random() < 0.9 else "img"}
+                 for _ in range(int(rng.integers(0, 7)))]
+        recs.append(f"http://s{i % 250}.org/\t" + json.dumps({"url": "x", "content": {"links": links}}))
+    inp = tmp_path / "cc.tsv"
+    inp.write_text("\n".join(recs) + "\n")
+    res = subprocess.run([CLI, str(inp), "10", "--format=ccjson"], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    hist = oracle(sparky_rdd.pairs_from_ccjson_lines(recs), 10)
+    got = parse_has_rank(res.stdout)
+    assert got.keys() == hist[-1].keys()
+    err = max(abs(got[u] - v) / v for u, v in hist[-1].items())
+    assert err <= 1e-9
+
+
+def test_cli_rejects_bad_input(tmp_path):
+    inp = tmp_path / "bad.txt"
+    inp.write_text("a b c\n")
+    res = subprocess.run([CLI, str(inp)], capture_output=True, text=True, timeout=60)
+    assert res.returncode != 0 and "tokens" in res.stderr
