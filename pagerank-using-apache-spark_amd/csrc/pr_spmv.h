@@ -117,6 +117,12 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
     if constexpr (MASK_GATHER) c = (int32_t)((uint32_t)c & gather_mask);
     if constexpr (XCLASS > 1)  // diagnostics only: emulate XCLASS column-line classes per XCD
       c = (c & ~((XCLASS - 1) << 4)) | (int32_t)((blockIdx.x & (XCLASS - 1)) << 4);
+    if constexpr (XCLASS < 0) {  // diagnostics only: contiguous class regions by XCC id
+      constexpr int C = -XCLASS, SH = (C == 8) ? 3 : ((C == 4) ? 2 : 1);
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      c = (int32_t)((xcc & (C - 1)) * (uint32_t)(S_pad >> SH) + ((uint32_t)c >> SH));
+    }
     v[j] = (i0 + j < n) ? gather<GM>(cin, c) : 0.0;
   }
 

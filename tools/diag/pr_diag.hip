@@ -102,6 +102,9 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
       case 13: launch<8, true, false, 3, 8>(g, L, mask); break;
       case 14: launch<8, true, false, 0, 2>(g, L, mask); break;
       case 15: launch<8, true, false, 0, 4>(g, L, mask); break;
+      case 16: launch<8, true, false, 0, -8>(g, L, mask); break;
+      case 17: launch<8, true, false, 0, -4>(g, L, mask); break;
+      case 18: launch<8, true, false, 0, -2>(g, L, mask); break;
       default: return fail(PR_ERR_INVALID, "unknown variant");
     }
   }
