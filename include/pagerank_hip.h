@@ -42,6 +42,8 @@ extern "C" {
 #define PR_DANGLING_NONE 1u  /* cluster-mode semantics: dangUrls empty on the driver, dc=0 */
 #define PR_INPUT_DEVICE 2u   /* src/dst are device pointers on `device` (not host)        */
 #define PR_NO_CANONICAL 4u   /* drop the canonical CSR after the build (no export)        */
+#define PR_LAYOUT_FUSED 8u   /* force the single-pass layout (default: chosen by size)    */
+#define PR_LAYOUT_SPLIT 16u  /* force the per-XCD column-class layout                     */
 
 /* ---- vertex flag bits (pr_graph_export_csr vflags) ---------------------------------- */
 #define PR_VF_KEY 1u    /* vertex is a record key / src          Sparky.java:127-135      */
@@ -63,7 +65,8 @@ extern "C" {
 #define PR_INFO_N_UNITS 10     /* work units of the SpMV launch                             */
 #define PR_INFO_N_LONG_ROWS 11 /* rows split across several units                          */
 #define PR_INFO_DEVICE_BYTES 12
-#define PR_INFO_COUNT 13
+#define PR_INFO_CLASSES 13     /* column classes of the layout (1 = fused single pass)     */
+#define PR_INFO_COUNT 14
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

@@ -56,7 +56,7 @@ int exchange(pr_graph *g, int buf) {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + degf.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + lens.bytes + partial.bytes + sunits.bytes + seg_row.bytes + seg_cls.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes;
   return b;
@@ -95,7 +95,9 @@ int create_common(int32_t device, int32_t part, int32_t n_parts, int32_t n_verti
   if (n_parts < 1 || part < 0 || part >= n_parts) return fail(PR_ERR_INVALID, "bad part / n_parts");
   if (n_vertices < 0 || n_edges < 0) return fail(PR_ERR_INVALID, "negative size");
   if (n_edges > 0 && (!src || !dst)) return fail(PR_ERR_INVALID, "src/dst is NULL");
-  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL)) return fail(PR_ERR_INVALID, "unknown flag bits");
+  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT))
+    return fail(PR_ERR_INVALID, "unknown flag bits");
+  if ((flags & PR_LAYOUT_FUSED) && (flags & PR_LAYOUT_SPLIT)) return fail(PR_ERR_INVALID, "PR_LAYOUT_FUSED and PR_LAYOUT_SPLIT are exclusive");
   PR_TRY(check_device(device));
   DeviceGuard dg(device);
   pr_graph *g = new (std::nothrow) pr_graph();
@@ -155,7 +157,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
-                                    g->n_units,   g->n_long,   (int64_t)g->device_bytes()};
+                                    g->n_units + g->n_sunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }
@@ -203,11 +205,12 @@ int pr_get_ranks(pr_graph *g, double *ranks_out) {
   if (!g || !ranks_out) return fail(PR_ERR_INVALID, "NULL argument");
   if (!g->ready) return fail(PR_ERR_STATE, "pr_get_ranks before pr_reset");
   DeviceGuard dg(g->device);
-  std::vector<double> loc((size_t)g->n_local);
-  if (g->n_local > 0)
-    PR_HIP(hipMemcpyAsync(loc.data(), g->r.p, sizeof(double) * g->n_local, hipMemcpyDeviceToHost, g->stream));
+  std::vector<double> loc((size_t)g->n_rows);
+  if (g->n_rows > 0)
+    PR_HIP(hipMemcpyAsync(loc.data(), g->r.p, sizeof(double) * g->n_rows, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
-  for (int64_t j = 0; j < g->n_local; ++j) ranks_out[g->orig_of_local[j]] = loc[j];
+  for (int64_t L = 0; L < g->n_rows; ++L)
+    if (g->orig_of_local[L] >= 0) ranks_out[g->orig_of_local[L]] = loc[L];
   return PR_OK;
 }
 

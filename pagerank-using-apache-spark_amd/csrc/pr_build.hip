@@ -112,23 +112,32 @@ __global__ void k_vflags(int32_t V, const uint8_t *__restrict__ is_key,
   atomicMax(&cnt[4], mo);
 }
 
-// Internal order key: out-degree descending, original ID ascending.
-__global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
-                             uint64_t *__restrict__ vk) {
+// Internal order key: heavy before light (split layout only), then out-degree descending,
+// original ID ascending.  *n_light counts the light vertices.
+__global__ void k_order_keys(int32_t V, int b, int bd, uint64_t maxd, bool split,
+                             const int32_t *__restrict__ deg, const int64_t *__restrict__ rowptr,
+                             uint64_t *__restrict__ vk, unsigned long long *__restrict__ n_light) {
+  unsigned long long nl = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * blockDim.x)
-    vk[v] = ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
+       v += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t light = (split && rowptr[v + 1] - rowptr[v] < kHeavyMinIndeg) ? 1ull : 0ull;
+    nl += light;
+    vk[v] = (light << (b + bd)) | ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
+  }
+  atomicAdd(n_light, nl);
 }
 
-// rank_of[v] = sorted index; gpos[v] = gather position of v's contribution.
-__global__ void k_rank_gpos(int32_t V, uint64_t mask, int P, int64_t S_pad,
+// rank_of[v] = sorted index; gpos[v] = gather position of v's contribution.  Sorted index i
+// -> part i % P, local rank j = i / P -> class x = j % C, q = j / C -> local row L = x*Q_pad + q.
+__global__ void k_rank_gpos(int32_t V, uint64_t mask, int P, int C, int64_t Q_pad, int64_t S_pad,
                             const uint64_t *__restrict__ sorted_vk, int32_t *__restrict__ rank_of,
                             int32_t *__restrict__ gpos) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t v = (int32_t)(sorted_vk[i] & mask);
     rank_of[v] = (int32_t)i;
-    gpos[v] = (int32_t)((i % P) * S_pad + i / P);
+    const int64_t j = i / P;
+    gpos[v] = (int32_t)((i % P) * S_pad + (j % C) * Q_pad + j / C);
   }
 }
 
@@ -141,18 +150,52 @@ struct PartPred {
     return rank_of[d] % P == part;
   }
 };
+// local key = (segment << (brow + bg)) | (row << bg) | gather position of src, where the
+// segment is the class of the source for a heavy destination row (row = heavy index h) and C
+// for a light one (row = local row L).
 struct PartXform {
   const uint64_t *k;
-  const int32_t *rank_of;
   const int32_t *gpos;
-  int b, P, bg;
+  int b, bg, brow;
   uint64_t mask;
+  ClassGeom geo;
   __device__ uint64_t operator()(int64_t i) const {
     const uint64_t key = k[i];
     const int32_t d = (int32_t)(key >> b), s = (int32_t)(key & mask);
-    return ((uint64_t)(rank_of[d] / P) << bg) | (uint64_t)(uint32_t)gpos[s];
+    const int64_t gs = gpos[s];
+    const int64_t L = gpos[d] % geo.S_pad;
+    const int64_t xd = L / geo.Q_pad, qd = L % geo.Q_pad;
+    uint64_t seg = (uint64_t)geo.C, row = (uint64_t)L;
+    if (geo.C > 1 && qd < geo.hcum[xd + 1] - geo.hcum[xd]) {
+      seg = (uint64_t)((gs % geo.S_pad) / geo.Q_pad);
+      row = (uint64_t)(geo.hcum[xd] + qd);
+    }
+    return (seg << (brow + bg)) | (row << bg) | (uint64_t)gs;
   }
 };
+
+// row_ptr over rows [0, R) of keys[lo, hi) whose row is (key >> shift) & rmask.
+__global__ void k_row_ptr_seg(const uint64_t *__restrict__ keys, int64_t lo, int64_t hi, int shift,
+                              uint64_t rmask, int64_t R, int64_t *__restrict__ row_ptr) {
+  const int64_t m = hi - lo;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t rc = (i < m) ? (int64_t)((keys[lo + i] >> shift) & rmask) : R;
+    const int64_t rp = (i > 0) ? (int64_t)((keys[lo + i - 1] >> shift) & rmask) : -1;
+    for (int64_t v = rp + 1; v <= rc; ++v) row_ptr[v] = i;
+  }
+}
+
+// Class boundaries of the sorted local keys: cls_start[x] = first key of class >= x.
+__global__ void k_class_bounds(const uint64_t *__restrict__ keys, int64_t m, int shift, int C,
+                               int64_t *__restrict__ cls_start) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= m;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t xc = (i < m) ? (int64_t)(keys[i] >> shift) : C;
+    const int64_t xp = (i > 0) ? (int64_t)(keys[i - 1] >> shift) : -1;
+    for (int64_t x = xp + 1; x <= xc; ++x) cls_start[x] = i;
+  }
+}
 
 __global__ void k_local_col(const uint64_t *__restrict__ keys, int64_t m, uint64_t mask,
                             int32_t *__restrict__ col) {
@@ -161,31 +204,55 @@ __global__ void k_local_col(const uint64_t *__restrict__ keys, int64_t m, uint64
     col[i] = (int32_t)(keys[i] & mask);
 }
 
-__global__ void k_local_rows(int64_t n_local, int P, int part, uint64_t mask, bool dangling_none,
-                             const uint64_t *__restrict__ sorted_vk, const int32_t *__restrict__ deg,
-                             const uint8_t *__restrict__ vflags, int32_t *__restrict__ degf,
-                             int32_t *__restrict__ orig) {
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n_local;
-       j += (int64_t)gridDim.x * blockDim.x) {
+// Per local row L: rowinfo (out-degree | RI_* flags) and the original ID (-1 for holes).
+__global__ void k_local_rows(int64_t R, int64_t n_local, int P, int part, ClassGeom geo,
+                             uint64_t mask, bool dangling_none, const uint64_t *__restrict__ sorted_vk,
+                             const int32_t *__restrict__ deg, const uint8_t *__restrict__ vflags,
+                             uint32_t *__restrict__ rowinfo, int32_t *__restrict__ orig) {
+  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R;
+       L += (int64_t)gridDim.x * blockDim.x) {
+    const int C = geo.C;
+    const int64_t x = L / geo.Q_pad, q = L % geo.Q_pad, j = q * C + x;
+    if (j >= n_local) {
+      rowinfo[L] = kRowHole;
+      orig[L] = -1;
+      continue;
+    }
     const int32_t v = (int32_t)(sorted_vk[j * P + part] & mask);
-    orig[j] = v;
-    const int32_t d = deg[v];
-    int32_t f = d;
-    if (d == 0) f = ((vflags[v] & PR_VF_SINK) && !dangling_none) ? -1 : 0;
-    degf[j] = f;
+    orig[L] = v;
+    uint32_t info = (uint32_t)deg[v];
+    if (deg[v] == 0 && (vflags[v] & PR_VF_SINK) && !dangling_none) info |= kRowSink;
+    if (vflags[v] & PR_VF_INDEG0) info |= kRowIndeg0;
+    if (C > 1 && q < geo.hcum[x + 1] - geo.hcum[x]) info |= kRowHeavy;
+    rowinfo[L] = info;
+  }
+}
+
+__global__ void k_lens(const int64_t *__restrict__ rp, int64_t R, uint16_t *__restrict__ lens) {
+  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R;
+       L += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = rp[L + 1] - rp[L];
+    lens[L] = (uint16_t)(l > kUnitNnz ? 0xFFFF : l);
   }
 }
 
 }  // namespace
 
 // Greedy work plan over the part's row_ptr (host; linear, deterministic).
-void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan) {
-  const int64_t R = (int64_t)rp.size() - 1;
-  int64_t pieces = 0, pad = 0, v = 0;
-  plan->units.clear();
-  plan->src_off.clear();
-  plan->lr_row.clear();
-  plan->lr_p0.clear();
+void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan,
+                int64_t row_begin, int64_t row_end, bool append) {
+  const int64_t R = row_end < 0 ? (int64_t)rp.size() - 1 : row_end;
+  if (!append) {
+    plan->units.clear();
+    plan->src_off.clear();
+    plan->lr_row.clear();
+    plan->lr_p0.clear();
+    plan->n_pieces = 0;
+    plan->padded_len = 0;
+  } else if (!plan->lr_p0.empty()) {
+    plan->lr_p0.pop_back();  // re-appended at the end
+  }
+  int64_t pieces = plan->n_pieces, pad = plan->padded_len, v = row_begin;
   auto push = [&](int64_t src, int32_t r0, int32_t meta, int32_t n) {
     plan->units.push_back(Unit{(uint32_t)(pad / 8), r0, meta, n});
     plan->src_off.push_back(src);
@@ -225,7 +292,8 @@ __global__ void k_pad_cols(const Unit *__restrict__ units, const int64_t *__rest
                            const int32_t *__restrict__ col, int32_t *__restrict__ colp) {
   const Unit u = units[blockIdx.x];
   const int64_t s = src_off[blockIdx.x], d = (int64_t)u.p8 * 8;
-  for (int i = threadIdx.x; i < u.n; i += blockDim.x) colp[d + i] = col[s + i];
+  const int n = unit_n(u);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) colp[d + i] = col[s + i];
 }
 }  // namespace
 
@@ -246,6 +314,7 @@ int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, h
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
+  static_assert(kClasses >= 1 && kClasses <= 16, "class count");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -335,87 +404,205 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   // ---- internal order: out-degree desc, ID asc (hot contributions first) ----
   g->n_local_max = (V + P - 1) / P;
   g->n_local = V > part ? (V - part + P - 1) / P : 0;
-  g->S_pad = ((g->n_local_max + 2 + 63) / 64) * 64;
+  if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
+  // Column classes: one per XCD when the part's contribution slice outgrows the L2s (pr_graph.h).
+  int C = (g->n_local_max * 8 > kSplitMinSliceBytes) ? kClasses : 1;
+  if (g->flags & PR_LAYOUT_FUSED) C = 1;
+  if (g->flags & PR_LAYOUT_SPLIT) C = kClasses;
+  g->C = C;
+  g->Q_pad = (g->n_local_max + C - 1) / C;
+  if (g->Q_pad < 1) g->Q_pad = 1;
+  g->n_rows = (int64_t)C * g->Q_pad;
+  g->S_pad = ((g->n_rows + 2 + 63) / 64) * 64;
+  if ((int64_t)P * g->S_pad >= (int64_t(1) << 31)) return fail(PR_ERR_INVALID, "gather space exceeds 2^31 entries");
   const int bd = bits_for(max_outdeg);
   const uint64_t maxd = (uint64_t(1) << bd) - 1;
-  DevBuf vk, vtmp, rank_of, gpos;
+  DevBuf vk, vtmp, rank_of, gpos, nlight;
   PR_TRY(vk.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
   PR_TRY(vtmp.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
   PR_TRY(rank_of.alloc(sizeof(int32_t) * ((size_t)V + 1)));
   PR_TRY(gpos.alloc(sizeof(int32_t) * ((size_t)V + 1)));
+  PR_TRY(nlight.alloc(sizeof(unsigned long long)));
+  PR_HIP(hipMemsetAsync(nlight.p, 0, sizeof(unsigned long long), s));
+  unsigned long long n_light = 0;
   if (V > 0) {
-    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, b, maxd,
-                       c_deg.as<int32_t>(), vk.as<uint64_t>());
-    PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd, s));
-    hipLaunchKernelGGL(k_rank_gpos, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, maskb, P,
-                       g->S_pad, vk.as<uint64_t>(), rank_of.as<int32_t>(), gpos.as<int32_t>());
+    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, bd, maxd, C > 1,
+                       c_deg.as<int32_t>(), c_rowptr.as<int64_t>(), vk.as<uint64_t>(),
+                       nlight.as<unsigned long long>());
+    PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd + 1, s));
+    hipLaunchKernelGGL(k_rank_gpos, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, maskb, P, C,
+                       g->Q_pad, g->S_pad, vk.as<uint64_t>(), rank_of.as<int32_t>(), gpos.as<int32_t>());
     PR_HIP(hipGetLastError());
+    PR_HIP(hipMemcpyAsync(&n_light, nlight.p, sizeof(n_light), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
   }
   vtmp.reset();
+  // heavy vertices sort first: part p owns sorted ranks i = p, p+P, ...; its heavy local ranks are
+  // j < Hp, and class x gets the heavy prefix q < H_x of its region
+  ClassGeom geo{};
+  geo.C = C;
+  geo.Q_pad = g->Q_pad;
+  geo.S_pad = g->S_pad;
+  {
+    const int64_t H_total = C > 1 ? (int64_t)V - (int64_t)n_light : 0;  // fused: no heavy rows
+    const int64_t Hp = H_total > part ? (H_total - part + P - 1) / P : 0;
+    geo.hcum[0] = 0;
+    for (int x = 0; x < C; ++x) geo.hcum[x + 1] = geo.hcum[x] + (Hp > x ? (Hp - x + C - 1) / C : 0);
+    for (int x = C; x < kClasses; ++x) geo.hcum[x + 1] = geo.hcum[x];
+  }
+  g->geo = geo;
+  g->n_heavy = geo.hcum[C];
 
-  // ---- the part's in-link CSR in gather positions ----
+  // ---- the part's in-link CSRs: one per class over heavy rows, one over light rows ----
+  const int64_t R = g->n_rows, H = g->n_heavy;
   const int bg = bits_for((uint64_t)P * g->S_pad);
+  const int brow = bits_for((uint64_t)R);
+  const int bseg = bits_for((uint64_t)C + 1);
   const uint64_t maskg = (uint64_t(1) << bg) - 1;
   int64_t lm = 0;
   PR_TRY(compact_index(m, PartPred{ukeys, rank_of.as<int32_t>(), b, P, part},
-                       PartXform{ukeys, rank_of.as<int32_t>(), gpos.as<int32_t>(), b, P, bg, maskb},
+                       PartXform{ukeys, gpos.as<int32_t>(), b, bg, brow, maskb, geo},
                        keys.as<uint64_t>(), &lm, s));
   g->local_nnz = lm;
-  const int brow = bits_for((uint64_t)(g->n_local > 0 ? g->n_local : 1));
-  PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, 0, bg + brow, s));
-  PR_TRY(g->rowptr.alloc(sizeof(int64_t) * ((size_t)g->n_local + 1)));
+  PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, 0, bg + brow + bseg, s));
   PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 ? lm : 1)));
-  hipLaunchKernelGGL(k_row_ptr, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s, keys.as<uint64_t>(),
-                     lm, bg, g->n_local, g->rowptr.as<int64_t>());
   if (lm > 0)
     hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
                        keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
-  PR_TRY(g->degf.alloc(sizeof(int32_t) * ((size_t)g->n_local + 1)));
+  DevBuf cls_start;
+  PR_TRY(cls_start.alloc(sizeof(int64_t) * (C + 2)));
+  hipLaunchKernelGGL(k_class_bounds, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s,
+                     keys.as<uint64_t>(), lm, bg + brow, C + 1, cls_start.as<int64_t>());
+  std::vector<int64_t> hcls(C + 2);
+  PR_HIP(hipMemcpyAsync(hcls.data(), cls_start.p, sizeof(int64_t) * (C + 2), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  PR_TRY(g->rowinfo.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
   DevBuf orig;
-  PR_TRY(orig.alloc(sizeof(int32_t) * ((size_t)g->n_local + 1)));
-  if (g->n_local > 0)
-    hipLaunchKernelGGL(k_local_rows, dim3(grid_for(g->n_local, T, 65536)), dim3(T), 0, s, g->n_local,
-                       P, part, maskb, (g->flags & PR_DANGLING_NONE) != 0, vk.as<uint64_t>(),
-                       c_deg.as<int32_t>(), c_vflags.as<uint8_t>(), g->degf.as<int32_t>(),
-                       orig.as<int32_t>());
+  PR_TRY(orig.alloc(sizeof(int32_t) * ((size_t)R + 1)));
+  hipLaunchKernelGGL(k_local_rows, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, g->n_local, P, part,
+                     geo, maskb, (g->flags & PR_DANGLING_NONE) != 0, vk.as<uint64_t>(),
+                     c_deg.as<int32_t>(), c_vflags.as<uint8_t>(), g->rowinfo.as<uint32_t>(),
+                     orig.as<int32_t>());
   PR_HIP(hipGetLastError());
-  keys.reset();
-  tmp.reset();
   vk.reset();
   rank_of.reset();
   gpos.reset();
 
-  // ---- work plan (host greedy over the part's row_ptr) + padded gather-position array ----
-  std::vector<int64_t> rp((size_t)g->n_local + 1);
-  g->orig_of_local.resize((size_t)g->n_local);
-  PR_HIP(hipMemcpyAsync(rp.data(), g->rowptr.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
-  if (g->n_local > 0)
-    PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * g->n_local,
-                          hipMemcpyDeviceToHost, s));
-  PR_HIP(hipStreamSynchronize(s));
-  UnitPlan plan;
-  plan_units(rp, kUnitNnz, kUnitRows, &plan);
-  if (plan.padded_len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
-  g->n_units = (int64_t)plan.units.size();
-  g->n_long = (int64_t)plan.lr_row.size();
-  g->n_pieces = plan.n_pieces;
-  PR_TRY(g->colp.alloc(sizeof(int32_t) * (plan.padded_len > 0 ? plan.padded_len : 8)));
-  PR_TRY(build_padded_cols(plan, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
-  g->col.reset();  // the unpadded copy is not needed by the iteration
-  PR_TRY(g->units.alloc(sizeof(Unit) * (plan.units.size() + 1)));
-  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * (plan.units.size() + 1)));
-  PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (plan.lr_row.size() + 1)));
-  PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (plan.lr_p0.size() + 1)));
+  // ---- work plans (host greedy) + one padded gather-position array for all units ----
+  UnitPlan all;  // src offsets / padded offsets of every unit, for build_padded_cols
+  const uint64_t rmask = (uint64_t(1) << brow) - 1;
+  DevBuf rp_dev;
+  PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
+  std::vector<int64_t> rp;
+  std::vector<std::vector<Unit>> cls_units(C);
+  std::vector<int32_t> seg_cls, seg_row, seg_p0;
+  std::vector<Unit> light_units;
+  std::vector<int32_t> lr_row, lr_p0;
+  int64_t pieces = 0, padded = 0;
+  if (C > 1) PR_TRY(g->lens.alloc(sizeof(uint16_t) * (size_t)C * (H + 1)));
+  auto absorb = [&](const UnitPlan &px, int64_t src_base, int cls, std::vector<Unit> &dst_units) {
+    for (size_t k = 0; k < px.units.size(); ++k) {
+      Unit u = px.units[k];
+      if (u.meta < 0) u.meta -= (int32_t)pieces;  // global piece index
+      u.p8 += (uint32_t)(padded / 8);
+      u.n |= cls << 16;
+      dst_units.push_back(u);
+      all.units.push_back(u);
+      all.src_off.push_back(px.src_off[k] + src_base);
+    }
+  };
+  for (int x = 0; x <= C; ++x) {
+    const bool light = (x == C);
+    const int64_t lo = hcls[x], hi = hcls[x + 1], rows = light ? R : H;
+    if (!light && (C == 1 || H == 0)) continue;
+    hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(hi - lo + 1, T, 65536)), dim3(T), 0, s,
+                       keys.as<uint64_t>(), lo, hi, bg, rmask, rows, rp_dev.as<int64_t>());
+    if (!light)
+      hipLaunchKernelGGL(k_lens, dim3(grid_for(rows, T, 65536)), dim3(T), 0, s, rp_dev.as<int64_t>(), rows,
+                         g->lens.as<uint16_t>() + (size_t)x * (H + 1));
+    PR_HIP(hipGetLastError());
+    rp.assign((size_t)rows + 1, 0);
+    PR_HIP(hipMemcpyAsync(rp.data(), rp_dev.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
+    UnitPlan px;
+    if (light) {
+      PR_TRY(g->rowptr.alloc(sizeof(int64_t) * ((size_t)R + 1)));
+      PR_HIP(hipMemcpyAsync(g->rowptr.p, rp_dev.p, sizeof(int64_t) * ((size_t)R + 1), hipMemcpyDeviceToDevice, s));
+      // light rows: region y's rows after its heavy prefix (holes are planned too, at no cost)
+      for (int y = 0; y < C; ++y)
+        plan_units(rp, kUnitNnz, kUnitRows, &px, (int64_t)y * g->Q_pad + (geo.hcum[y + 1] - geo.hcum[y]),
+                   (int64_t)(y + 1) * g->Q_pad, true);
+      for (size_t q = 0; q + 1 < px.lr_p0.size(); ++q) {
+        lr_row.push_back(px.lr_row[q]);
+        lr_p0.push_back((int32_t)(px.lr_p0[q] + pieces));
+      }
+      absorb(px, lo, 0, light_units);
+    } else {
+      plan_units(rp, kUnitNnz, kUnitRows, &px);
+      for (size_t q = 0; q + 1 < px.lr_p0.size(); ++q) {
+        seg_cls.push_back(x);
+        seg_row.push_back(px.lr_row[q]);
+        seg_p0.push_back((int32_t)(px.lr_p0[q] + pieces));
+      }
+      absorb(px, lo, x, cls_units[x]);
+    }
+    pieces += px.n_pieces;
+    padded += px.padded_len;
+  }
+  seg_p0.push_back((int32_t)pieces);
+  lr_p0.push_back((int32_t)pieces);
+  keys.reset();
+  tmp.reset();
+  all.padded_len = padded;
+  all.n_pieces = pieces;
+  if (all.padded_len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+  PR_TRY(g->colp.alloc(sizeof(int32_t) * (all.padded_len > 0 ? all.padded_len : 8)));
+  PR_TRY(build_padded_cols(all, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
+  g->col.reset();
+  // class units launch at position k*C + x, so blockIdx % 8 == x: one XCD per class under the
+  // observed round-robin placement (any placement stays correct, only slower)
+  std::vector<Unit> order;
+  if (C > 1) {
+    size_t mx = 0;
+    for (auto &v : cls_units) mx = std::max(mx, v.size());
+    order.resize(mx * C, Unit{0, 0, 0, 0});
+    for (int x = 0; x < C; ++x)
+      for (size_t k = 0; k < mx; ++k)
+        order[k * C + x] = k < cls_units[x].size() ? cls_units[x][k] : Unit{0, 0, 0, x << 16};
+  }
+  g->n_sunits = (int64_t)order.size();
+  g->n_units = (int64_t)light_units.size();
+  g->n_long = (int64_t)lr_row.size();
+  g->n_segs = (int64_t)seg_row.size();
+  g->n_pieces = pieces;
+  PR_TRY(g->units.alloc(sizeof(Unit) * (light_units.size() + 1)));
+  PR_TRY(g->sunits.alloc(sizeof(Unit) * (order.size() + 1)));
+  PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (lr_row.size() + 1)));
+  PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (lr_p0.size() + 1)));
+  PR_TRY(g->seg_row.alloc(sizeof(int32_t) * (seg_row.size() + 1)));
+  PR_TRY(g->seg_cls.alloc(sizeof(int32_t) * (seg_cls.size() + 1)));
+  PR_TRY(g->seg_p0.alloc(sizeof(int32_t) * (seg_p0.size() + 1)));
   PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
-  if (!plan.units.empty())
-    PR_HIP(hipMemcpyAsync(g->units.p, plan.units.data(), sizeof(Unit) * plan.units.size(), hipMemcpyHostToDevice, s));
-  if (!plan.lr_row.empty())
-    PR_HIP(hipMemcpyAsync(g->lr_row.p, plan.lr_row.data(), sizeof(int32_t) * plan.lr_row.size(), hipMemcpyHostToDevice, s));
-  PR_HIP(hipMemcpyAsync(g->lr_p0.p, plan.lr_p0.data(), sizeof(int32_t) * plan.lr_p0.size(), hipMemcpyHostToDevice, s));
+  if (!light_units.empty())
+    PR_HIP(hipMemcpyAsync(g->units.p, light_units.data(), sizeof(Unit) * light_units.size(), hipMemcpyHostToDevice, s));
+  if (!order.empty())
+    PR_HIP(hipMemcpyAsync(g->sunits.p, order.data(), sizeof(Unit) * order.size(), hipMemcpyHostToDevice, s));
+  if (!lr_row.empty())
+    PR_HIP(hipMemcpyAsync(g->lr_row.p, lr_row.data(), sizeof(int32_t) * lr_row.size(), hipMemcpyHostToDevice, s));
+  PR_HIP(hipMemcpyAsync(g->lr_p0.p, lr_p0.data(), sizeof(int32_t) * lr_p0.size(), hipMemcpyHostToDevice, s));
+  if (!seg_row.empty()) {
+    PR_HIP(hipMemcpyAsync(g->seg_row.p, seg_row.data(), sizeof(int32_t) * seg_row.size(), hipMemcpyHostToDevice, s));
+    PR_HIP(hipMemcpyAsync(g->seg_cls.p, seg_cls.data(), sizeof(int32_t) * seg_cls.size(), hipMemcpyHostToDevice, s));
+  }
+  PR_HIP(hipMemcpyAsync(g->seg_p0.p, seg_p0.data(), sizeof(int32_t) * seg_p0.size(), hipMemcpyHostToDevice, s));
+  if (C > 1) PR_TRY(g->partial.alloc(sizeof(double) * (size_t)C * (H > 0 ? H : 1)));
+  g->orig_of_local.resize((size_t)R);
+  if (R > 0)
+    PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * R, hipMemcpyDeviceToHost, s));
   PR_HIP(hipStreamSynchronize(s));
 
   // ---- iteration state ----
-  PR_TRY(g->r.alloc(sizeof(double) * ((size_t)g->n_local + 1)));
+  PR_TRY(g->r.alloc(sizeof(double) * ((size_t)g->n_rows + 1)));
   for (int k = 0; k < 2; ++k) {
     PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)P * g->S_pad));
     PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)P * g->S_pad, s));
@@ -424,7 +611,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->fin_part.alloc(sizeof(double) * 2 * g->fin_blocks));
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
-  g->reset_blocks = (int)grid_for(g->n_local > 0 ? g->n_local : 1, 256, 2048);
+  g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
+  g->ep_blocks = (int)grid_for(g->n_heavy > 0 ? g->n_heavy : 1, 256, 2048);
+  // finalize input: light-unit partials followed by the split epilogue's block partials
+  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 
   if (g->flags & PR_NO_CANONICAL) {

@@ -11,8 +11,17 @@
 //   rowptr  int64[n_local+1]  in-link CSR of the part's rows (local row order)
 //   colp    int32[padded nnz]  gather positions, ascending within a row, grouped by work unit,
 //                             every unit 32-byte aligned (pr_spmv.h loads them as int4)
-//   degf    int32[n_local]    out-degree d>0; 0 = key without links; -1 = sink-only (in D)
-//   r       fp64[n_local]     ranks, updated in place
+//   rowinfo uint32[R]         out-degree | kRowSink (in D) | kRowIndeg0 | kRowHole
+//   r       fp64[R]           ranks, updated in place
+//
+// Column classes (C = 8 once a part's contribution slice exceeds the L2s, else C = 1): local
+// rank j -> class j % C; a slice is C contiguous regions of Q_pad rows, so row L = x*Q_pad + q is
+// also the gather position inside the slice (holes pad the last region).  In-links are split by
+// the class of their source; class-x work units run at blockIdx % 8 == x, i.e. on one XCD, whose
+// 4 MiB L2 then caches only class-x contributions (8x the aggregate L2 reach for the gathers).
+// Only heavy rows (>= kHeavyMinIndeg in-links; a prefix of every region, since heavy vertices
+// sort first) are split: heavy row h has C partial slots partial[x][h] that an epilogue pass
+// adds in class order.  Light rows keep the fused single pass (pr_spmv.h k_spmv_units).
 //   cbuf    fp64[2][P*S_pad]  contributions r/d, double-buffered across iterations
 #pragma once
 
@@ -30,7 +39,10 @@ struct pr_graph {
   int32_t V = 0;          // N = totalUrlCount
   int64_t E_dedup = 0;    // E'
   int part = 0, nparts = 1;
-  int64_t n_local = 0;      // rows owned
+  int64_t n_local = 0;      // rows owned (without holes)
+  int64_t n_rows = 0;       // C * Q_pad local rows (with holes)
+  int C = 1;                // column classes
+  int64_t Q_pad = 0;        // rows per class region
   int64_t n_local_max = 0;  // ceil(V / P)
   int64_t S_pad = 0;        // doubles per gather slice
   int64_t local_nnz = 0;
@@ -44,7 +56,11 @@ struct pr_graph {
   bool has_canonical = false;
 
   // part layout
-  pr::DevBuf rowptr, col, colp, degf, r;
+  pr::DevBuf rowptr, col, colp, rowinfo, r;
+  pr::DevBuf lens, partial, sunits, seg_row, seg_cls, seg_p0;
+  int ep_blocks = 0;
+  pr::ClassGeom geo{};
+  int64_t n_heavy = 0, n_sunits = 0, n_segs = 0;
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;

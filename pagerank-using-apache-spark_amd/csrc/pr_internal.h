@@ -84,9 +84,37 @@ struct Unit {
   uint32_t p8;   // padded column offset / 8
   int32_t r0;    // first row (STREAM) or the long row (PIECE)
   int32_t meta;  // rows (>= 0) or -(piece index + 1)
-  int32_t n;     // in-links in the unit
+  int32_t n;     // in-links in the unit (low 16 bits) | column class << 16
 };
 static_assert(sizeof(Unit) == 16, "Unit must stay 16 bytes");
+__host__ __device__ inline int unit_n(const Unit &u) { return u.n & 0xFFFF; }
+__host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
+
+// ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
+constexpr int kClasses = 8;                          // one per XCD of the MI355X
+constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once c outgrows the 8 x 4 MiB L2s
+
+// per-row info word: out-degree | flags
+constexpr uint32_t kRowDegMask = (1u << 28) - 1;
+constexpr uint32_t kRowSink = 1u << 28;    // in the dangling set D (contributes to dc)
+constexpr uint32_t kRowIndeg0 = 1u << 29;  // no in-link: the old rank is the sum
+constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
+constexpr uint32_t kRowHeavy = 1u << 31;   // class-split row (its sum comes from the epilogue)
+// Only rows with at least this many in-links are split by class: a split row costs C partial
+// slots (write + read) and C row lengths, worth it only when enough gathers gain L2 locality.
+constexpr int kHeavyMinIndeg = 8;
+
+// Geometry of the split layout of one part, passed to kernels by value.
+struct ClassGeom {
+  int C;
+  int64_t Q_pad, S_pad;
+  int64_t hcum[kClasses + 1];  // heavy rows in regions < x (heavy rows are a prefix of a region)
+  __host__ __device__ int64_t heavy_to_row(int64_t h) const {
+    int y = 0;
+    while (y + 1 < C && hcum[y + 1] <= h) ++y;
+    return (int64_t)y * Q_pad + (h - hcum[y]);
+  }
+};
 
 // Host plan over a part's row_ptr: units, their source offsets in the unpadded column array,
 // long rows (split into pieces) and the padded column length.
@@ -97,7 +125,9 @@ struct UnitPlan {
   int64_t n_pieces = 0;
   int64_t padded_len = 0;
 };
-void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan);
+// Plans rows [row_begin, row_end) (default: all rows); appends to *plan when append is true.
+void plan_units(const std::vector<int64_t> &rp, int unit_nnz, int unit_rows, UnitPlan *plan,
+                int64_t row_begin = 0, int64_t row_end = -1, bool append = false);
 // colp[8*p8 + i] = col[src_off + i] for every unit (padding entries are 0).
 int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, hipStream_t s);
 

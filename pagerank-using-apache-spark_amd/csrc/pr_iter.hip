@@ -43,7 +43,7 @@ __device__ __forceinline__ double load_sc1(const double *p) {
 __global__ __launch_bounds__(kThreads) void k_finalize(
     int64_t n_long, const int32_t *__restrict__ lr_row, const int32_t *__restrict__ lr_p0,
     const double *__restrict__ piece_part, const double2 *__restrict__ parts, int64_t n_parts,
-    double *__restrict__ r, const int32_t *__restrict__ degf, const double *__restrict__ cin,
+    double *__restrict__ r, const uint32_t *__restrict__ rowinfo, const double *__restrict__ cin,
     double *__restrict__ cout, int P, int64_t S_pad, double n_vertices, double teleport,
     double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
     double *__restrict__ slot_out) {
@@ -64,9 +64,10 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
         const double rold = r[v];
         const double rn = affine(acc, tdc, teleport, damping);
         r[v] = rn;
-        const int32_t df = degf[v];
-        if (df > 0) cout[v] = __ddiv_rn(rn, (double)df);
-        else if (df < 0) dcp = __dadd_rn(dcp, rn);
+        const uint32_t info = rowinfo[v];
+        const uint32_t d = info & kRowDegMask;
+        if (d > 0) cout[v] = __ddiv_rn(rn, (double)d);
+        else if (info & kRowSink) dcp = __dadd_rn(dcp, rn);
         l1p = __dadd_rn(l1p, fabs(rn - rold));
       }
     }
@@ -101,20 +102,25 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_reset(int64_t n_local, const double *__restrict__ init,
+__global__ __launch_bounds__(kThreads) void k_reset(int64_t n_rows, const double *__restrict__ init,
                                                     double *__restrict__ r,
-                                                    const int32_t *__restrict__ degf,
+                                                    const uint32_t *__restrict__ rowinfo,
                                                     double *__restrict__ cout,
                                                     double2 *__restrict__ parts) {
   __shared__ double red[kThreads / kWave];
   double dcp = 0.0;
-  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < n_local;
+  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < n_rows;
        j += (int64_t)gridDim.x * kThreads) {
+    const uint32_t info = rowinfo[j];
+    if (info & kRowHole) {
+      r[j] = 0.0;
+      continue;
+    }
     const double x = init ? init[j] : 1.0;  // Sparky.java:165-170
     r[j] = x;
-    const int32_t df = degf[j];
-    if (df > 0) cout[j] = __ddiv_rn(x, (double)df);
-    else if (df < 0) dcp = __dadd_rn(dcp, x);
+    const uint32_t d = info & kRowDegMask;
+    if (d > 0) cout[j] = __ddiv_rn(x, (double)d);
+    else if (info & kRowSink) dcp = __dadd_rn(dcp, x);
   }
   dcp = block_sum<kThreads>(dcp, red);
   if (threadIdx.x == 0) parts[blockIdx.x] = make_double2(dcp, 0.0);
@@ -135,7 +141,7 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
   double *cout = g->cbuf[out_buf].as<double>() + own;
   hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, g->stream, n_long,
                      g->lr_row.as<int32_t>(), g->lr_p0.as<int32_t>(), g->piece_part.as<double>(),
-                     parts, n_parts, g->r.as<double>(), g->degf.as<int32_t>(),
+                     parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[in_buf].as<double>(), cout, g->nparts, g->S_pad, (double)g->V,
                      g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
                      cout + g->S_pad - 2);
@@ -148,17 +154,18 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 int iter_reset(pr_graph *g, const double *init_host) {
   hipStream_t s = g->stream;
   DevBuf dinit;
-  if (init_host && g->n_local > 0) {
-    std::vector<double> loc((size_t)g->n_local);
-    for (int64_t j = 0; j < g->n_local; ++j) loc[j] = init_host[g->orig_of_local[j]];
-    PR_TRY(dinit.alloc(sizeof(double) * g->n_local));
-    PR_HIP(hipMemcpyAsync(dinit.p, loc.data(), sizeof(double) * g->n_local, hipMemcpyHostToDevice, s));
+  if (init_host && g->n_rows > 0) {
+    std::vector<double> loc((size_t)g->n_rows, 0.0);
+    for (int64_t L = 0; L < g->n_rows; ++L)
+      if (g->orig_of_local[L] >= 0) loc[L] = init_host[g->orig_of_local[L]];
+    PR_TRY(dinit.alloc(sizeof(double) * g->n_rows));
+    PR_HIP(hipMemcpyAsync(dinit.p, loc.data(), sizeof(double) * g->n_rows, hipMemcpyHostToDevice, s));
     PR_HIP(hipStreamSynchronize(s));
   }
   g->cur = 0;
   const int64_t own = (int64_t)g->part * g->S_pad;
-  hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_local,
-                     dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->degf.as<int32_t>(),
+  hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
+                     dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
   PR_HIP(hipGetLastError());
   PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0));
@@ -184,19 +191,38 @@ int iter_compute(pr_graph *g) {
     if (!e0 || !e1) return fail(PR_ERR_HIP, "hipEventCreate failed");
     PR_HIP(hipEventRecord(e0, s));
   }
+  // light rows (all rows when C == 1): fused single pass
   if (g->n_units > 0)
     hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
                        g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
-                       g->degf.as<int32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
+                       g->rowinfo.as<uint32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
                        g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
+  int64_t n_parts = g->n_units;
+  if (g->C > 1 && g->n_heavy > 0) {  // heavy rows: per-class sums, then the epilogue
+    const int64_t H = g->n_heavy;
+    if (g->n_sunits > 0)
+      hipLaunchKernelGGL((k_spmv_split<kPerThread, true>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0, s,
+                         g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
+                         g->cbuf[in].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(), H,
+                         0xFFFFFFFFu);
+    if (g->n_segs > 0)
+      hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
+                         g->n_segs, g->seg_row.as<int32_t>(), g->seg_cls.as<int32_t>(), g->seg_p0.as<int32_t>(),
+                         g->piece_part.as<double>(), g->partial.as<double>(), H);
+    hipLaunchKernelGGL(k_epilogue<kClasses>, dim3(g->ep_blocks), dim3(kThreads), 0, s, H, g->geo,
+                       g->partial.as<double>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
+                       g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->nparts,
+                       (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);
+    n_parts += g->ep_blocks;
+  }
   PR_HIP(hipGetLastError());
   if (g->timing) {
     PR_HIP(hipEventRecord(e1, s));
     const int base = (int)g->ev_next - 2;
     g->spmv_ev.push_back({base, base + 1});
   }
-  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units, in, out));
+  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), n_parts, in, out));
   g->cur = out;
   ++g->iters_done;
   return PR_OK;

@@ -70,7 +70,7 @@ template <int PT, bool NT, bool MASK_GATHER = false, int GM = 0, int XCLASS = 0>
 __global__ __launch_bounds__(kThreads) void k_spmv_units(
     const Unit *__restrict__ units, const int64_t *__restrict__ rowptr,
     const int32_t *__restrict__ colp, const double *__restrict__ cin, double *__restrict__ cout,
-    double *__restrict__ r, const int32_t *__restrict__ degf, double *__restrict__ piece_part,
+    double *__restrict__ r, const uint32_t *__restrict__ rowinfo, double *__restrict__ piece_part,
     double2 *__restrict__ unit_part, int P, int64_t S_pad, double n_vertices, double teleport,
     double damping, uint32_t gather_mask) {
   __shared__ double rowsum[kUnitRows];
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
 
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
   const Unit u = units[blockIdx.x];
-  const int n = u.n;
+  const int n = unit_n(u);
   const int i0 = t * PT;
   const bool stream = u.meta >= 0;
   const int nr = stream ? u.meta : 0;
@@ -100,12 +100,12 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
   }
   int64_t rp_t = 0;
   double rold0 = 0.0;
-  int32_t df0 = 0;
+  uint32_t info0 = 0;
   if (stream) {
     if (t <= nr) rp_t = rowptr[r0 + t];
     if (t < nr) {
       rold0 = r[(int64_t)r0 + t];
-      df0 = degf[(int64_t)r0 + t];
+      info0 = rowinfo[(int64_t)r0 + t];
     }
   }
 
@@ -231,16 +231,230 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
   for (int k = t; k < nr; k += kThreads) {
     const int64_t vtx = (int64_t)r0 + k;
     const double rold = (k == t) ? rold0 : r[vtx];
-    const int32_t df = (k == t) ? df0 : degf[vtx];
+    const uint32_t info = (k == t) ? info0 : rowinfo[vtx];
+    if (info & (kRowHole | kRowHeavy)) continue;
     const double S = (lrp[k + 1] > lrp[k]) ? rowsum[k] : rold;
     const double rn = affine(S, tdc, teleport, damping);
     r[vtx] = rn;
-    if (df > 0) cout[vtx] = __ddiv_rn(rn, (double)df);
-    else if (df < 0) dcp = __dadd_rn(dcp, rn);
+    const uint32_t d = info & kRowDegMask;
+    if (d > 0) cout[vtx] = __ddiv_rn(rn, (double)d);
+    else if (info & kRowSink) dcp = __dadd_rn(dcp, rn);
     l1p = __dadd_rn(l1p, fabs(rn - rold));
   }
   const double2 part = block_sum2<kThreads>(make_double2(dcp, l1p), red2);
   if (t == 0) unit_part[blockIdx.x] = part;
+}
+
+// ============================================================================================
+// Split layout (C column classes, pr_graph.h): per-class row sums, then one epilogue pass.
+// ============================================================================================
+
+// Walk + segmented scan shared by both STREAM paths: every thread sums its PT values along the
+// unit's row boundaries (lrp in LDS); completed row sums land in rowsum[] (LDS).
+template <int PT>
+__device__ __forceinline__ void stream_row_sums(const double (&v)[PT], int n, int nr, const int32_t *lrp,
+                                                double *rowsum, int32_t *wrow_first, int32_t *wrow_last,
+                                                double *wval_last) {
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int i0 = t * PT;
+  int carry_row = -1, first_row = -1;
+  double carry_val = 0.0, first_sum = 0.0;
+  if (i0 < n) {
+    int lo = 0, hi = nr + 1;  // first k with lrp[k] > i0
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lrp[mid] <= i0) lo = mid + 1;
+      else hi = mid;
+    }
+    int cur = lo - 1;
+    const int kstart = cur;
+    const bool started_before = lrp[cur] < i0;
+    int next_end = lrp[cur + 1];
+    double acc = 0.0;
+    bool open = false;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      if (i0 + j < n) {
+        acc = __dadd_rn(acc, v[j]);
+        open = true;
+        if (i0 + j + 1 == next_end) {
+          if (cur == kstart && started_before) {
+            first_row = cur;
+            first_sum = acc;
+          } else {
+            rowsum[cur] = acc;
+          }
+          acc = 0.0;
+          open = false;
+          ++cur;
+          while (cur < nr && lrp[cur + 1] == lrp[cur]) ++cur;
+          next_end = (cur < nr) ? lrp[cur + 1] : INT_MAX;
+        }
+      }
+    }
+    if (open) {
+      carry_row = cur;
+      carry_val = acc;
+    }
+  }
+  int srow = carry_row;
+  double sval = carry_val;
+#pragma unroll
+  for (int off = 1; off < kWave; off <<= 1) {
+    const int prow = __shfl_up(srow, off, kWave);
+    const double pval = __shfl_up(sval, off, kWave);
+    if (lane >= off && srow >= 0 && prow == srow) sval = __dadd_rn(pval, sval);
+  }
+  const int lane0_row = __shfl(carry_row, 0, kWave);
+  if (lane == kWave - 1) {
+    wrow_last[w] = srow;
+    wval_last[w] = sval;
+    wrow_first[w] = lane0_row;
+  }
+  __syncthreads();
+  int prow_in = -1;
+  double pval_in = 0.0;
+  for (int ww = 0; ww < w; ++ww) {
+    const int rl = wrow_last[ww];
+    const bool full = (rl >= 0) && (wrow_first[ww] == rl);
+    if (full && prow_in == rl) {
+      pval_in = __dadd_rn(pval_in, wval_last[ww]);
+    } else {
+      prow_in = rl;
+      pval_in = (rl >= 0) ? wval_last[ww] : 0.0;
+    }
+  }
+  if (srow >= 0 && srow == prow_in && lane0_row == srow) sval = __dadd_rn(pval_in, sval);
+  int erow = __shfl_up(srow, 1, kWave);
+  double eval = __shfl_up(sval, 1, kWave);
+  if (lane == 0) {
+    erow = prow_in;
+    eval = pval_in;
+  }
+  if (first_row >= 0) rowsum[first_row] = (erow == first_row) ? __dadd_rn(eval, first_sum) : first_sum;
+  __syncthreads();
+}
+
+// Class-x work unit (launched at blockIdx % 8 == x): gathers only class-x contributions and
+// writes partial[x][row] for every row of the unit (0 for rows without class-x in-links).
+template <int PT, bool NT, bool MASK_GATHER = false>
+__global__ __launch_bounds__(kThreads) void k_spmv_split(
+    const Unit *__restrict__ units, const uint16_t *__restrict__ lens, const int32_t *__restrict__ colp,
+    const double *__restrict__ cin, double *__restrict__ partial, double *__restrict__ piece_part,
+    int64_t R, uint32_t gather_mask = 0xFFFFFFFFu) {
+  static_assert(kUnitRows <= 4 * kThreads, "lens scan covers 4 rows per thread");
+  __shared__ double rowsum[kUnitRows];
+  __shared__ int32_t lrp[kUnitRows + 1];
+  __shared__ double red[kThreads / kWave];
+  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
+  __shared__ double wval_last[kThreads / kWave];
+  __shared__ uint32_t scan_scratch[kThreads / kWave];
+
+  const int t = threadIdx.x;
+  const Unit u = units[blockIdx.x];
+  const int n = unit_n(u), x = unit_cls(u);
+  if (u.meta == 0) return;  // empty padding unit (or a unit of zero rows)
+  const int i0 = t * PT;
+  const bool stream = u.meta > 0;
+  const int nr = stream ? u.meta : 0;
+  const int32_t r0 = u.r0;
+
+  int32_t ci[PT];
+  if (i0 < n) {
+    load_cols<PT, NT>(colp + (int64_t)u.p8 * 8 + i0, ci);
+  } else {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) ci[j] = 0;
+  }
+  uint32_t l4[4] = {0, 0, 0, 0};
+  if (stream) {  // streamed once per iteration: non-temporal, keep the L2 for contributions
+    const uint16_t *lx = lens + (int64_t)x * (R + 1) + r0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * t + q < nr) l4[q] = __builtin_nontemporal_load(lx + 4 * t + q);
+  }
+  double v[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    int32_t c = ci[j];
+    if constexpr (MASK_GATHER) c = (int32_t)((uint32_t)c & gather_mask);  // diagnostics only
+    v[j] = (i0 + j < n) ? cin[c] : 0.0;
+  }
+
+  if (!stream) {  // PIECE of a long (row, class) segment
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) acc = __dadd_rn(acc, v[j]);
+    acc = block_sum<kThreads>(acc, red);
+    if (t == 0) piece_part[-u.meta - 1] = acc;
+    return;
+  }
+
+  // unit-local row pointers from the class's uint16 row lengths
+  uint32_t tot;
+  const uint32_t base = block_exclusive_scan<kThreads>(l4[0] + l4[1] + l4[2] + l4[3], scan_scratch, &tot);
+  {
+    uint32_t acc = base;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (4 * t + q < nr) lrp[4 * t + q] = (int32_t)acc;
+      acc += l4[q];
+    }
+    if (t == 0) lrp[nr] = (int32_t)tot;
+  }
+  __syncthreads();
+  stream_row_sums<PT>(v, n, nr, lrp, rowsum, wrow_first, wrow_last, wval_last);
+  double *px = partial + (int64_t)x * R + r0;
+  for (int k = t; k < nr; k += kThreads)
+    __builtin_nontemporal_store((lrp[k + 1] > lrp[k]) ? rowsum[k] : 0.0, px + k);
+}
+
+// Long (row, class) segments: the sum of their pieces in piece order -> partial[x][row].
+__global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const int32_t *__restrict__ seg_row,
+                                                         const int32_t *__restrict__ seg_cls,
+                                                         const int32_t *__restrict__ seg_p0,
+                                                         const double *__restrict__ piece_part,
+                                                         double *__restrict__ partial, int64_t R) {
+  const int lane = lane_id();
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t q = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); q < n_seg; q += nw) {
+    const int32_t p0 = seg_p0[q], np = seg_p0[q + 1] - p0;
+    double acc = 0.0;
+    for (int k = lane; k < np; k += kWave) acc = __dadd_rn(acc, piece_part[p0 + k]);
+    acc = wave_sum(acc);
+    if (lane == 0) partial[(int64_t)seg_cls[q] * R + seg_row[q]] = acc;
+  }
+}
+
+// Epilogue of the split layout over the heavy rows h: S = sum of the C class partials in class
+// order (heavy rows always have in-links), then the fused update of k_spmv_units.
+template <int C>
+__global__ __launch_bounds__(kThreads) void k_epilogue(int64_t H, ClassGeom geo, const double *__restrict__ partial,
+                                                       const uint32_t *__restrict__ rowinfo,
+                                                       double *__restrict__ r, double *__restrict__ cout,
+                                                       const double *__restrict__ cin, int P,
+                                                       double n_vertices, double teleport, double damping,
+                                                       double2 *__restrict__ ep_part) {
+  __shared__ double2 red2[kThreads / kWave];
+  const double tdc = dc_from_slots(cin, P, geo.S_pad) / n_vertices;
+  double dcp = 0.0, l1p = 0.0;
+  for (int64_t h = (int64_t)blockIdx.x * kThreads + threadIdx.x; h < H; h += (int64_t)gridDim.x * kThreads) {
+    const int64_t L = geo.heavy_to_row(h);
+    const uint32_t info = rowinfo[L];
+    const double rold = r[L];
+    double S = __builtin_nontemporal_load(partial + h);
+#pragma unroll
+    for (int x = 1; x < C; ++x) S = __dadd_rn(S, __builtin_nontemporal_load(partial + (int64_t)x * H + h));
+    if (info & kRowIndeg0) S = rold;
+    const double rn = affine(S, tdc, teleport, damping);
+    r[L] = rn;
+    const uint32_t d = info & kRowDegMask;
+    if (d > 0) cout[L] = __ddiv_rn(rn, (double)d);
+    else if (info & kRowSink) dcp = __dadd_rn(dcp, rn);
+    l1p = __dadd_rn(l1p, fabs(rn - rold));
+  }
+  const double2 part = block_sum2<kThreads>(make_double2(dcp, l1p), red2);
+  if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
 }  // namespace pr

@@ -52,10 +52,11 @@ class PageRankGraph:
 
     def __init__(self, n_vertices: int, src, dst, *, device: int = 0, dangling: str = "local",
                  part: int = 0, n_parts: int = 1, keep_canonical: bool = True,
-                 device_input: bool = False, n_edges: Optional[int] = None):
+                 device_input: bool = False, n_edges: Optional[int] = None, layout: str = "auto"):
         """src/dst: int32 host arrays (numpy) of raw interned edges, dst == -1 for a record
         without links; or, with device_input=True, integer device addresses (e.g. from
-        torch ``tensor.data_ptr()``) plus n_edges."""
+        torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (column classes once the
+        contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h)."""
         L = _lib.load()
         flags = 0
         if dangling == "none":
@@ -64,6 +65,12 @@ class PageRankGraph:
             raise ValueError("dangling must be 'local' or 'none'")
         if not keep_canonical:
             flags |= _lib.PR_NO_CANONICAL
+        if layout == "fused":
+            flags |= _lib.PR_LAYOUT_FUSED
+        elif layout == "split":
+            flags |= _lib.PR_LAYOUT_SPLIT
+        elif layout != "auto":
+            raise ValueError("layout must be 'auto', 'fused' or 'split'")
         if device_input:
             flags |= _lib.PR_INPUT_DEVICE
             if n_edges is None:

@@ -38,10 +38,12 @@ def assert_csr_equal(g, csr):
     assert np.array_equal(ex.vflags, csr.vflags)
 
 
-def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None):
+def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, layout="auto"):
     csr = oracle_c.build_csr(V, src, dst)
     ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
-    with hip.PageRankGraph(V, src, dst, dangling=dangling) as g:
+    with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout) as g:
+        if layout != "auto":
+            assert g.info()["classes"] == (1 if layout == "fused" else 8)
         assert_csr_equal(g, csr)
         hist = []
         ranks, stats = g.run(iters, init_ranks=init, want_ranks_in_callback=True,
@@ -95,18 +97,20 @@ def random_edges(rng, V, E, p_nolink=0.05, hub_frac=0.0):
     return src.astype(np.int32), dst.astype(np.int32)
 
 
+@pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("V,E,seed", [(1, 1, 0), (17, 60, 1), (1000, 9000, 2), (50000, 800000, 3)])
-def test_random_graphs(hip, oracle_c, V, E, seed):
+def test_random_graphs(hip, oracle_c, V, E, seed, layout):
     rng = np.random.default_rng(seed)
     src, dst = random_edges(rng, V, E)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10, layout=layout)
     for it in range(10):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
         assert abs(stats[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
         assert abs(stats[it].l1_delta - ref["l1"][it]) <= 1e-9 * max(ref["l1"][it], 1.0)
 
 
-def test_long_rows_and_unit_boundaries(hip, oracle_c):
+@pytest.mark.parametrize("layout", ["fused", "split"])
+def test_long_rows_and_unit_boundaries(hip, oracle_c, layout):
     """Hubs split into many 2048-in-link pieces, rows of exactly 2048 / 2049 in-links, and a
     run of > 1024 short rows (the per-unit row cap)."""
     rng = np.random.default_rng(9)
@@ -119,27 +123,33 @@ def test_long_rows_and_unit_boundaries(hip, oracle_c):
     parts_d.append(100 + (np.arange(V) + 7) % (V - 100))  # ring over non-hub rows
     src = np.concatenate(parts_s).astype(np.int32)
     dst = np.concatenate(parts_d).astype(np.int32)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 8)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 8, layout=layout)
     indeg = np.diff(csr.row_ptr)
     assert indeg[1] == 2048 and indeg[2] == 2049 and indeg[4] == 2047
-    assert info["n_long_rows"] == int(np.sum(indeg > 2048)) == 4  # 70000, 2049, 4096, 6144
+    if layout == "fused":
+        assert info["n_long_rows"] == int(np.sum(indeg > 2048)) == 4  # 70000, 2049, 4096, 6144
+    else:  # long (row, class) segments: the 70000-in-link hub splits into 8 long segments
+        assert info["n_long_rows"] >= 8
     assert info["max_indeg"] == 70000
     for it in range(8):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
-def test_heavy_hub_and_many_indeg0(hip, oracle_c):
+@pytest.mark.parametrize("layout", ["fused", "split"])
+def test_heavy_hub_and_many_indeg0(hip, oracle_c, layout):
     rng = np.random.default_rng(4)
     src, dst = random_edges(rng, 20000, 300000, p_nolink=0.2, hub_frac=0.3)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 20000, src, dst, 10)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 20000, src, dst, 10, layout=layout)
     assert info["max_indeg"] > 15000  # ~90k raw in-links from 20k sources collapse (A1)
     assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
 
 
-def test_dangling_none(hip, oracle_c):
+@pytest.mark.parametrize("layout", ["fused", "split"])
+def test_dangling_none(hip, oracle_c, layout):
     rng = np.random.default_rng(5)
     src, dst = random_edges(rng, 3000, 20000)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 3000, src, dst, 10, dangling="none")
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, 3000, src, dst, 10, dangling="none",
+                                                  layout=layout)
     assert all(s.dangling_sum == 0.0 for s in stats)
     assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
 
@@ -154,13 +164,14 @@ def test_resume_from_saved_ranks(hip, oracle_c):
     assert max_rel(r3_2, r5) <= 1e-13
 
 
-def test_deterministic_bitwise(hip):
+@pytest.mark.parametrize("layout", ["fused", "split"])
+def test_deterministic_bitwise(hip, layout):
     rng = np.random.default_rng(7)
     src, dst = random_edges(rng, 40000, 600000, hub_frac=0.05)
-    with hip.PageRankGraph(40000, src, dst) as g:
+    with hip.PageRankGraph(40000, src, dst, layout=layout) as g:
         a, _ = g.run(10)
         b, _ = g.run(10)
-    with hip.PageRankGraph(40000, src, dst) as g2:
+    with hip.PageRankGraph(40000, src, dst, layout=layout) as g2:
         c, _ = g2.run(10)
     assert np.array_equal(a, b) and np.array_equal(a, c)
 
@@ -218,8 +229,9 @@ def host_first_appearance(src, dst):
     return labels.size, s2.astype(np.int32), d2.astype(np.int32)
 
 
-@pytest.mark.parametrize("gen,scale,ef", [("rmat", 14, 16), ("er", 13, 16), ("rmat", 18, 16)])
-def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef):
+@pytest.mark.parametrize("gen,scale,ef,layout", [("rmat", 14, 16, "auto"), ("er", 13, 16, "auto"),
+                                                  ("rmat", 18, 16, "fused"), ("rmat", 18, 16, "split")])
+def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef, layout):
     import torch
 
     E = ef << scale
@@ -240,7 +252,7 @@ def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef):
     # graph from device-resident edges == graph from host edges == oracle
     csr = oracle_c.build_csr(V, hs, hd)
     ref = oracle_c.run(csr, 10)
-    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E) as g:
+    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, layout=layout) as g:
         assert_csr_equal(g, csr)
         r, st = g.run(10)
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
@@ -249,8 +261,9 @@ def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef):
     assert np.all(r >= 0.15)
 
 
+@pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("P", [2, 3, 4])
-def test_row_partition_group_on_one_gpu(hip, oracle_c, P):
+def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout):
     """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
     exchange is the group's device-copy all-gather (RCCL carries it across processes)."""
     rng = np.random.default_rng(30 + P)
@@ -258,7 +271,8 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P):
     src, dst = random_edges(rng, V, 500000, hub_frac=0.05)
     csr = oracle_c.build_csr(V, src, dst)
     ref = oracle_c.run(csr, 10)
-    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False) for p in range(P)]
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout=layout)
+             for p in range(P)]
     try:
         infos = [p.info() for p in parts]
         assert sum(i["local_rows"] for i in infos) == V

@@ -23,7 +23,7 @@ std::map<std::pair<pr_graph *, int>, std::unique_ptr<Layout>> g_layouts;
 __global__ void k_unpad(const Unit *__restrict__ units, const int64_t *__restrict__ src_off,
                         const int32_t *__restrict__ colp, int32_t *__restrict__ col) {
   const Unit u = units[blockIdx.x];
-  for (int i = threadIdx.x; i < u.n; i += blockDim.x) col[src_off[blockIdx.x] + i] = colp[(int64_t)u.p8 * 8 + i];
+  for (int i = threadIdx.x; i < unit_n(u); i += blockDim.x) col[src_off[blockIdx.x] + i] = colp[(int64_t)u.p8 * 8 + i];
 }
 
 int layout_for(pr_graph *g, int pt, Layout **out) {
@@ -31,7 +31,8 @@ int layout_for(pr_graph *g, int pt, Layout **out) {
   auto it = g_layouts.find(key);
   if (it != g_layouts.end()) { *out = it->second.get(); return PR_OK; }
   hipStream_t s = g->stream;
-  std::vector<int64_t> rp((size_t)g->n_local + 1);
+  if (g->C != 1) return fail(PR_ERR_STATE, "diag variants need the fused layout (PR_LAYOUT_FUSED)");
+  std::vector<int64_t> rp((size_t)g->n_rows + 1);
   PR_HIP(hipMemcpy(rp.data(), g->rowptr.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost));
   UnitPlan prod;
   plan_units(rp, kUnitNnz, kUnitRows, &prod);  // the product's plan: recover unpadded columns
@@ -65,7 +66,7 @@ void launch(pr_graph *g, Layout *L, uint32_t mask) {
   hipLaunchKernelGGL((k_spmv_units<PT, NT, MASK, GM, XC>), dim3((unsigned)L->n_units), dim3(kThreads), 0,
                      g->stream, L->units.as<Unit>(), g->rowptr.as<int64_t>(), L->colp.as<int32_t>(),
                      g->cbuf[0].as<double>(), g->cbuf[1].as<double>() + own, g->r.as<double>(),
-                     g->degf.as<int32_t>(), L->piece_part.as<double>(), L->unit_part.as<double2>(),
+                     g->rowinfo.as<uint32_t>(), L->piece_part.as<double>(), L->unit_part.as<double2>(),
                      g->nparts, g->S_pad, (double)g->V, 0.15, 0.85, mask);
 }
 
@@ -107,6 +108,38 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
       case 18: launch<8, true, false, 0, -2>(g, L, mask); break;
       default: return fail(PR_ERR_INVALID, "unknown variant");
     }
+  }
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipEventRecord(b, g->stream));
+  PR_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *ms_out = ms / iters;
+  return PR_OK;
+}
+
+// Split layout variants on the graph's own layout: 0 = product kernel, 1 = gathers masked by
+// `mask` (diagnostics: results wrong).
+int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
+  if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
+  PR_HIP(hipSetDevice(g->device));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  PR_HIP(hipEventRecord(a, g->stream));
+  for (int i = 0; i < iters; ++i) {
+    if (variant == 0)
+      hipLaunchKernelGGL((k_spmv_split<kPerThread, true, false>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0,
+                         g->stream, g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
+                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
+                         g->n_heavy, mask);
+    else
+      hipLaunchKernelGGL((k_spmv_split<kPerThread, true, true>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0,
+                         g->stream, g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
+                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
+                         g->n_heavy, mask);
   }
   PR_HIP(hipGetLastError());
   PR_HIP(hipEventRecord(b, g->stream));

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--graph", default="rmat")
     ap.add_argument("--variants", default="0,1,2,3,4:19,4:22,4:24")
+    ap.add_argument("--layout", default="fused", choices=["fused", "split"])
     a = ap.parse_args()
     import torch
 
@@ -32,7 +33,7 @@ def main():
         sparky_hip.gen_er(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=3)
     V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
     g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E,
-                                 keep_canonical=False)
+                                 keep_canonical=False, layout=a.layout)
     del s, d
     torch.cuda.empty_cache()
     info = g.info()
@@ -40,6 +41,8 @@ def main():
     D = ctypes.CDLL(os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpagerank_diag.so"))
     D.prd_time_spmv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double)]
+    D.prd_time_split.argtypes = D.prd_time_spmv.argtypes
+    fn = D.prd_time_split if a.layout == "split" else D.prd_time_spmv
     nbytes = 12 * info["local_edges"] + 36 * info["local_rows"]
     print(f"graph {a.graph} s{a.scale}: V={V} E'={info['n_edges']} units={info['n_units']} "
           f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
@@ -54,7 +57,7 @@ def main():
     for rnd in range(a.rounds):
         for v, m, t in variants:
             ms = ctypes.c_double()
-            rc = D.prd_time_spmv(g._h, v, m, a.iters, ctypes.byref(ms))
+            rc = fn(g._h, v, m, a.iters, ctypes.byref(ms))
             if rc != 0:
                 raise RuntimeError(f"variant {t}: rc={rc}")
             res[t].append(ms.value)

@@ -12,7 +12,9 @@ import json
 import os
 import sys
 
-KERNEL = "k_spmv_units"
+# the SpMV pass of one iteration = these kernels (pr_iter.hip iter_compute)
+PASS_KERNELS = ("k_spmv_units", "k_spmv_split", "k_seg_reduce", "k_epilogue")
+KERNEL = "k_spmv_"
 
 
 def rows(pattern):
@@ -23,14 +25,28 @@ def rows(pattern):
     return out
 
 
-def counter_per_launch(d, name):
+def counter_per_launch(d, name, kernels=(KERNEL,)):
     vals = {}
     for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
-        if KERNEL not in r.get("Kernel_Name", "") or r.get("Counter_Name") != name:
+        if not any(k in r.get("Kernel_Name", "") for k in kernels) or r.get("Counter_Name") != name:
             continue
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return sorted(vals.values())
+
+
+def counter_per_pass(d, name):
+    """Sum of the counter over the pass kernels / number of iterations (split or fused launches)."""
+    tot, iters = 0.0, set()
+    per = {}
+    for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
+        kn = r.get("Kernel_Name", "")
+        if not any(k in kn for k in PASS_KERNELS) or r.get("Counter_Name") != name:
+            continue
+        key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        per[(key, kn)] = per.get((key, kn), 0.0) + float(r["Counter_Value"])
+    n_iter = len({k for (k, kn) in per if "k_spmv_units" in kn}) or 1
+    return sum(per.values()) / n_iter if per else None
 
 
 def main():
@@ -60,6 +76,14 @@ def main():
     if fetch and write:
         res["hbm_bytes_per_launch"] = (2 * res["fetch_size_kb_median"] + res["write_size_kb_median"]) * 1024
         res["formula"] = "(2*FETCH_SIZE + WRITE_SIZE) * 1024, median over launches"
+    fp = counter_per_pass(os.path.join(d, "fetch"), "FETCH_SIZE")
+    wp = counter_per_pass(os.path.join(d, "write"), "WRITE_SIZE")
+    if fp is not None and wp is not None:
+        res["pass_fetch_kb"], res["pass_write_kb"] = fp, wp
+        res["hbm_bytes_per_pass"] = (2 * fp + wp) * 1024
+        res["pass_kernels"] = list(PASS_KERNELS)
+    res["trace_pass_kernels"] = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+                                 for r in stats if any(k in r.get("Name", "") for k in PASS_KERNELS)}
     print(json.dumps(res, indent=1))
     print(json.dumps(summary["kernels"][:12], indent=1))
     if out_json:
