@@ -61,8 +61,11 @@ def main():
     miss = counter_per_launch(os.path.join(d, "l2"), "TCC_MISS_sum")
     fetch = counter_per_launch(os.path.join(d, "fetch"), "FETCH_SIZE")
     write = counter_per_launch(os.path.join(d, "write"), "WRITE_SIZE")
+    import re
+    bench_src = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bench.py")).read()
     res = {
         "workload": f"R-MAT scale-{scale} edge-factor 16 (Graph500 .57/.19/.19, seed 2)",
+        "layout_version": re.search(r'LAYOUT_VERSION = "([^"]+)"', bench_src).group(1),
         "kernel": KERNEL,
         "trace_avg_ns": float(spmv[0]["AverageNs"]) if spmv else None,
         "trace_calls": int(spmv[0]["Calls"]) if spmv else None,
