@@ -409,6 +409,104 @@ __global__ __launch_bounds__(kThreads) void k_spmv_split(
     __builtin_nontemporal_store((lrp[k + 1] > lrp[k]) ? rowsum[k] : 0.0, px + k);
 }
 
+// Persistent form of k_spmv_split: gridDim (a multiple of 8) workgroups walk the unit list with
+// stride gridDim, so unit k still runs at blockIdx % 8 == k % 8 (its class's XCD).  While one
+// unit is reduced, the next unit's gather positions are already in flight (descriptor two units
+// ahead), hiding the HBM latency that bounds a one-unit-per-workgroup launch.
+template <int PT, bool NT>
+__device__ __forceinline__ void split_unit(const Unit &u, const int32_t (&ci)[PT], const uint16_t *__restrict__ lens,
+                                           const double *__restrict__ cin, double *__restrict__ partial,
+                                           double *__restrict__ piece_part, int64_t R, double *rowsum,
+                                           int32_t *lrp, double *red, int32_t *wrow_first, int32_t *wrow_last,
+                                           double *wval_last, uint32_t *scan_scratch) {
+  const int t = threadIdx.x;
+  const int n = unit_n(u), x = unit_cls(u);
+  const int i0 = t * PT;
+  const bool stream = u.meta > 0;
+  const int nr = stream ? u.meta : 0;
+  const int32_t r0 = u.r0;
+  uint32_t l4[4] = {0, 0, 0, 0};
+  if (stream) {
+    const uint16_t *lx = lens + (int64_t)x * (R + 1) + r0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (4 * t + q < nr) l4[q] = __builtin_nontemporal_load(lx + 4 * t + q);
+  }
+  double v[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) v[j] = (i0 + j < n) ? cin[ci[j]] : 0.0;
+  if (!stream) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) acc = __dadd_rn(acc, v[j]);
+    acc = block_sum<kThreads>(acc, red);
+    if (t == 0) piece_part[-u.meta - 1] = acc;
+    return;
+  }
+  uint32_t tot;
+  const uint32_t base = block_exclusive_scan<kThreads>(l4[0] + l4[1] + l4[2] + l4[3], scan_scratch, &tot);
+  {
+    uint32_t acc = base;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (4 * t + q < nr) lrp[4 * t + q] = (int32_t)acc;
+      acc += l4[q];
+    }
+    if (t == 0) lrp[nr] = (int32_t)tot;
+  }
+  __syncthreads();
+  stream_row_sums<PT>(v, n, nr, lrp, rowsum, wrow_first, wrow_last, wval_last);
+  double *px = partial + (int64_t)x * R + r0;
+  for (int k = t; k < nr; k += kThreads)
+    __builtin_nontemporal_store((lrp[k + 1] > lrp[k]) ? rowsum[k] : 0.0, px + k);
+  __syncthreads();  // rowsum / lrp are reused by the next unit
+}
+
+template <int PT, bool NT, int MINW = 1>
+__global__ __launch_bounds__(kThreads, MINW) void k_spmv_split_persist(
+    const Unit *__restrict__ units, int64_t n_units, const uint16_t *__restrict__ lens,
+    const int32_t *__restrict__ colp, const double *__restrict__ cin, double *__restrict__ partial,
+    double *__restrict__ piece_part, int64_t R) {
+  __shared__ double rowsum[kUnitRows];
+  __shared__ int32_t lrp[kUnitRows + 1];
+  __shared__ double red[kThreads / kWave];
+  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
+  __shared__ double wval_last[kThreads / kWave];
+  __shared__ uint32_t scan_scratch[kThreads / kWave];
+  const int64_t stride = gridDim.x;
+  int64_t k = blockIdx.x;
+  if (k >= n_units) return;
+  const int i0 = threadIdx.x * PT;
+  const Unit empty{0, 0, 0, 0};
+  Unit u = units[k];
+  Unit un = (k + stride < n_units) ? units[k + stride] : empty;
+  int32_t ci[PT];
+  if (i0 < unit_n(u)) load_cols<PT, NT>(colp + (int64_t)u.p8 * 8 + i0, ci);
+  else {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) ci[j] = 0;
+  }
+  while (true) {
+    const int64_t k1 = k + stride, k2 = k1 + stride;
+    int32_t ci1[PT];
+    if (k1 < n_units && i0 < unit_n(un)) load_cols<PT, NT>(colp + (int64_t)un.p8 * 8 + i0, ci1);
+    else {
+#pragma unroll
+      for (int j = 0; j < PT; ++j) ci1[j] = 0;
+    }
+    const Unit unn = (k2 < n_units) ? units[k2] : empty;
+    if (u.meta != 0)
+      split_unit<PT, NT>(u, ci, lens, cin, partial, piece_part, R, rowsum, lrp, red, wrow_first, wrow_last,
+                         wval_last, scan_scratch);
+    if (k1 >= n_units) break;
+    u = un;
+    un = unn;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) ci[j] = ci1[j];
+    k = k1;
+  }
+}
+
 // Long (row, class) segments: the sum of their pieces in piece order -> partial[x][row].
 __global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const int32_t *__restrict__ seg_row,
                                                          const int32_t *__restrict__ seg_cls,

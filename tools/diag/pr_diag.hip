@@ -130,7 +130,17 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   PR_HIP(hipEventCreate(&b));
   PR_HIP(hipEventRecord(a, g->stream));
   for (int i = 0; i < iters; ++i) {
-    if (variant == 0)
+    if (variant == 4)
+      hipLaunchKernelGGL((k_spmv_split_persist<kPerThread, true, 8>), dim3(2048), dim3(kThreads), 0,
+                         g->stream, g->sunits.as<Unit>(), g->n_sunits, g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
+                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
+                         g->n_heavy);
+    else if (variant == 2 || variant == 3)
+      hipLaunchKernelGGL((k_spmv_split_persist<kPerThread, true>), dim3(variant == 2 ? 1536 : 1024), dim3(kThreads), 0,
+                         g->stream, g->sunits.as<Unit>(), g->n_sunits, g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
+                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
+                         g->n_heavy);
+    else if (variant == 0)
       hipLaunchKernelGGL((k_spmv_split<kPerThread, true, false>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0,
                          g->stream, g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
                          g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
