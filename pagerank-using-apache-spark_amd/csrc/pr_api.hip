@@ -56,7 +56,7 @@ int exchange(pr_graph *g, int buf) {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + lens.bytes + partial.bytes + sunits.bytes + seg_row.bytes + seg_cls.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + seg_row.bytes + seg_cls.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes;
   return b;
@@ -157,7 +157,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
-                                    g->n_units + g->n_sunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C};
+                                    g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

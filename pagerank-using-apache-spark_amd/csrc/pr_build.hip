@@ -8,6 +8,7 @@
 //   dangUrls fixup           (:172-184)  -> D = sink-only vertices, resolved here once
 // then lays the part's rows out for the iteration (pr_graph.h) and plans the SpMV work units.
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <vector>
 
@@ -228,13 +229,6 @@ __global__ void k_local_rows(int64_t R, int64_t n_local, int P, int part, ClassG
   }
 }
 
-__global__ void k_lens(const int64_t *__restrict__ rp, int64_t R, uint16_t *__restrict__ lens) {
-  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R;
-       L += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t l = rp[L + 1] - rp[L];
-    lens[L] = (uint16_t)(l > kUnitNnz ? 0xFFFF : l);
-  }
-}
 
 }  // namespace
 
@@ -311,6 +305,158 @@ int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, h
   PR_HIP(hipGetLastError());
   PR_HIP(hipStreamSynchronize(s));
   return PR_OK;
+}
+
+// ---- heavy rows: wave units + entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) ----------------
+struct WavePlan {
+  std::vector<Unit> units;       // p8 = entry offset / 8, r0 = first heavy row, meta, n = padded entries
+  std::vector<int64_t> src_off;  // first in-link of the unit in its class's CSR
+  std::vector<int32_t> cls;
+  std::vector<int64_t> ucum;     // units of class < x
+  int64_t len = 0;               // entries (padded)
+};
+
+// Greedy, linear, deterministic: consecutive whole segments (empty ones count one dummy entry)
+// while they fit kWaveUnit entries; a segment longer than kWaveUnit becomes PIECE units.
+static void plan_wave_units(const std::vector<int64_t> &rp, int x, int pt, WavePlan *wp, int64_t *pieces,
+                            std::vector<int32_t> *seg_cls, std::vector<int32_t> *seg_row,
+                            std::vector<int32_t> *seg_p0) {
+  const int64_t H = (int64_t)rp.size() - 1, cap = (int64_t)kWave * pt;
+  auto push = [&](int64_t src, int64_t r0, int64_t meta, int64_t n) {
+    const int64_t np = (n + pt - 1) / pt * pt;
+    wp->units.push_back(Unit{(uint32_t)(wp->len / 8), (int32_t)r0, (int32_t)meta, (int32_t)np});
+    wp->src_off.push_back(src);
+    wp->cls.push_back(x);
+    wp->len += np;
+  };
+  int64_t h = 0;
+  while (h < H) {
+    const int64_t len = rp[h + 1] - rp[h];
+    if (len > cap) {
+      const int64_t np = (len + cap - 1) / cap;
+      seg_cls->push_back(x);
+      seg_row->push_back((int32_t)h);
+      seg_p0->push_back((int32_t)*pieces);
+      for (int64_t q = 0; q < np; ++q)
+        push(rp[h] + q * cap, h, -(*pieces + q) - 1, std::min<int64_t>(cap, len - q * cap));
+      *pieces += np;
+      ++h;
+      continue;
+    }
+    const int64_t start = h;
+    int64_t n = 0;
+    while (h < H) {
+      const int64_t l = rp[h + 1] - rp[h];
+      if (l > cap || n + std::max<int64_t>(l, 1) > cap) break;
+      n += std::max<int64_t>(l, 1);
+      ++h;
+    }
+    push(rp[start], start, h - start, n);
+  }
+}
+
+// Entry code (pr_internal.h); a segment end is marked in bit 0 until k_unit_meta moves it into
+// the lane metadata (codes are byte offsets / addresses, multiples of 8).
+__device__ __forceinline__ uint32_t hot_code(int32_t pos, int x, const HotGeom &hg, bool end) {
+  const int64_t p = pos / hg.S_pad, w = pos - p * hg.S_pad, y = w / hg.Q_pad, q = w - y * hg.Q_pad;
+  const uint32_t c = (y == x && q < hg.Kp) ? (uint32_t)(8 * (1 + p * hg.Kp + q)) : (kEntGlobal | ((uint32_t)pos * 8u));
+  return end ? (c | 1u) : c;
+}
+
+// One workgroup per wave unit: writes its entry codes (segment ends, dummies, padding).
+__global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, int cap, const Unit *__restrict__ units,
+                                                  const int64_t *__restrict__ src_off,
+                                                  const int32_t *__restrict__ ucls,
+                                                  const int64_t *__restrict__ rp_all, int64_t H,
+                                                  const int64_t *__restrict__ cls_lo,
+                                                  const int32_t *__restrict__ col, HotGeom hg,
+                                                  uint32_t *__restrict__ colh) {
+  __shared__ uint32_t scratch[256 / kWave];
+  const uint32_t zero = kEntZero;
+  for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
+    const Unit u = units[b];
+    const int x = ucls[b];
+    const int64_t *rp = rp_all + (int64_t)x * (H + 1);
+    const int32_t *cx = col + cls_lo[x];
+    uint32_t *dst = colh + (int64_t)u.p8 * 8;
+    const int npad = u.n;
+    if (u.meta < 0) {
+      const int64_t s0 = src_off[b];
+      const int64_t n = min((int64_t)cap, rp[u.r0 + 1] - s0);
+      for (int i = threadIdx.x; i < npad; i += 256) dst[i] = i < n ? hot_code(cx[s0 + i], x, hg, false) : zero;
+      continue;
+    }
+    const int nr = u.meta;  // <= cap <= 1024 rows: four per thread
+    const int r_a = 4 * threadIdx.x;
+    int64_t ln[4];
+    uint32_t ef[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = r_a + k;
+      ln[k] = r < nr ? rp[u.r0 + r + 1] - rp[u.r0 + r] : 0;
+      ef[k] = r < nr ? (uint32_t)max(ln[k], (int64_t)1) : 0u;
+      sum += ef[k];
+    }
+    uint32_t tot;
+    uint32_t off = block_exclusive_scan<256>(sum, scratch, &tot);
+    for (int k = 0; k < 4; ++k) {
+      const int r = r_a + k;
+      if (r >= nr) break;
+      const int64_t len = ln[k];
+      if (len == 0) {
+        dst[off] = zero | 1u;  // dummy: the row has no class-x in-link
+      } else {
+        const int64_t s0 = rp[u.r0 + r];
+        for (int64_t i = 0; i < len; ++i) dst[off + i] = hot_code(cx[s0 + i], x, hg, i == len - 1);
+      }
+      off += ef[k];
+    }
+    for (int i = (int)tot + threadIdx.x; i < npad; i += 256) dst[i] = zero;
+  }
+}
+
+// One wave per unit: moves the end marks into the lane metadata word (end mask, the static
+// predicates of the segmented scan, the lane's first segment index) and clears them in the codes.
+__global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *__restrict__ units,
+                                                  uint32_t *__restrict__ colh, uint32_t *__restrict__ meta) {
+  const int t = threadIdx.x;
+  for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
+    const Unit u = units[b];
+    uint32_t endm = 0;
+    int excl = 0;
+    uint32_t *c = colh + (int64_t)u.p8 * 8 + t * kWavePT;
+    const bool live = t * kWavePT < u.n;
+    for (int j = 0; j < kWavePT; ++j) {
+      const uint32_t v = live ? c[j] : 0u;
+      const bool e = u.meta >= 0 && (v & 1u);
+      endm |= (e ? 1u : 0u) << j;
+      const unsigned long long bm = __ballot(e);
+      excl += __popcll(bm & lanemask_lt());
+      if (live) c[j] = v & ~1u;
+    }
+    const unsigned long long F = __ballot(endm != 0);
+    // no segment end among lanes [lo, t]
+    auto clear = [&](int lo) -> bool {
+      const unsigned long long m = (t == 63 ? ~0ull : ((1ull << (t + 1)) - 1)) & ~((1ull << lo) - 1);
+      return (F & m) == 0;
+    };
+    uint32_t cond = 0;
+    const int r = t & 15, row = t >> 4;
+    for (int s = 0; s < 4; ++s) {
+      const int k = 1 << s;
+      if (r >= k && clear(t - k + 1)) cond |= 1u << s;
+    }
+    if ((row == 1 || row == 3) && clear(row * 16)) cond |= 1u << 4;
+    if (row >= 2 && clear(32)) cond |= 1u << 5;
+    meta[b * 64 + t] = endm | (cond * kMetaStep0) | ((uint32_t)excl << kMetaExclShift);
+  }
+}
+
+static int hot_slots_setting() {
+  int k = kHotSlotsDefault;
+  if (const char *e = getenv("PR_HOT_SLOTS")) k = atoi(e);  // tuning knob
+  const int max_slots = (160 * 1024) / 8 - 64;
+  return std::max(0, std::min(k, max_slots));
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
@@ -409,6 +555,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   int C = (g->n_local_max * 8 > kSplitMinSliceBytes) ? kClasses : 1;
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
   if (g->flags & PR_LAYOUT_SPLIT) C = kClasses;
+  // heavy-row entry codes are byte offsets below 2^31 (pr_internal.h)
+  if ((int64_t)P * (g->n_local_max + 64 + kClasses) * 8 >= (1ll << 31) - (1ll << 20)) C = 1;
   g->C = C;
   g->Q_pad = (g->n_local_max + C - 1) / C;
   if (g->Q_pad < 1) g->Q_pad = 1;
@@ -494,38 +642,29 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   DevBuf rp_dev;
   PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
   std::vector<int64_t> rp;
-  std::vector<std::vector<Unit>> cls_units(C);
   std::vector<int32_t> seg_cls, seg_row, seg_p0;
   std::vector<Unit> light_units;
   std::vector<int32_t> lr_row, lr_p0;
   int64_t pieces = 0, padded = 0;
-  if (C > 1) PR_TRY(g->lens.alloc(sizeof(uint16_t) * (size_t)C * (H + 1)));
-  auto absorb = [&](const UnitPlan &px, int64_t src_base, int cls, std::vector<Unit> &dst_units) {
-    for (size_t k = 0; k < px.units.size(); ++k) {
-      Unit u = px.units[k];
-      if (u.meta < 0) u.meta -= (int32_t)pieces;  // global piece index
-      u.p8 += (uint32_t)(padded / 8);
-      u.n |= cls << 16;
-      dst_units.push_back(u);
-      all.units.push_back(u);
-      all.src_off.push_back(px.src_off[k] + src_base);
-    }
-  };
+  // heavy rows: per-class row pointers stay on the device for the code fill
+  WavePlan wp;
+  DevBuf rp_all;
+  if (C > 1 && H > 0) PR_TRY(rp_all.alloc(sizeof(int64_t) * (size_t)C * (H + 1)));
   for (int x = 0; x <= C; ++x) {
     const bool light = (x == C);
     const int64_t lo = hcls[x], hi = hcls[x + 1], rows = light ? R : H;
+    if (!light) wp.ucum.push_back((int64_t)wp.units.size());
+    else seg_p0.push_back((int32_t)pieces);  // end of the heavy pieces
     if (!light && (C == 1 || H == 0)) continue;
+    int64_t *rpd = light ? rp_dev.as<int64_t>() : rp_all.as<int64_t>() + (size_t)x * (H + 1);
     hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(hi - lo + 1, T, 65536)), dim3(T), 0, s,
-                       keys.as<uint64_t>(), lo, hi, bg, rmask, rows, rp_dev.as<int64_t>());
-    if (!light)
-      hipLaunchKernelGGL(k_lens, dim3(grid_for(rows, T, 65536)), dim3(T), 0, s, rp_dev.as<int64_t>(), rows,
-                         g->lens.as<uint16_t>() + (size_t)x * (H + 1));
+                       keys.as<uint64_t>(), lo, hi, bg, rmask, rows, rpd);
     PR_HIP(hipGetLastError());
     rp.assign((size_t)rows + 1, 0);
-    PR_HIP(hipMemcpyAsync(rp.data(), rp_dev.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipMemcpyAsync(rp.data(), rpd, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
     PR_HIP(hipStreamSynchronize(s));
-    UnitPlan px;
     if (light) {
+      UnitPlan px;
       PR_TRY(g->rowptr.alloc(sizeof(int64_t) * ((size_t)R + 1)));
       PR_HIP(hipMemcpyAsync(g->rowptr.p, rp_dev.p, sizeof(int64_t) * ((size_t)R + 1), hipMemcpyDeviceToDevice, s));
       // light rows: region y's rows after its heavy prefix (holes are planned too, at no cost)
@@ -536,47 +675,77 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
         lr_row.push_back(px.lr_row[q]);
         lr_p0.push_back((int32_t)(px.lr_p0[q] + pieces));
       }
-      absorb(px, lo, 0, light_units);
-    } else {
-      plan_units(rp, kUnitNnz, kUnitRows, &px);
-      for (size_t q = 0; q + 1 < px.lr_p0.size(); ++q) {
-        seg_cls.push_back(x);
-        seg_row.push_back(px.lr_row[q]);
-        seg_p0.push_back((int32_t)(px.lr_p0[q] + pieces));
+      for (size_t k = 0; k < px.units.size(); ++k) {
+        Unit u = px.units[k];
+        if (u.meta < 0) u.meta -= (int32_t)pieces;  // global piece index
+        light_units.push_back(u);
+        all.units.push_back(u);
+        all.src_off.push_back(px.src_off[k] + lo);
       }
-      absorb(px, lo, x, cls_units[x]);
+      pieces += px.n_pieces;
+      padded += px.padded_len;
+    } else {
+      plan_wave_units(rp, x, kWavePT, &wp, &pieces, &seg_cls, &seg_row, &seg_p0);
     }
-    pieces += px.n_pieces;
-    padded += px.padded_len;
   }
-  seg_p0.push_back((int32_t)pieces);
+  wp.ucum.resize(kClasses + 1, (int64_t)wp.units.size());
   lr_p0.push_back((int32_t)pieces);
   keys.reset();
   tmp.reset();
   all.padded_len = padded;
   all.n_pieces = pieces;
-  if (all.padded_len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+  if (all.padded_len / 8 >= (int64_t(1) << 32) || wp.len / 8 >= (int64_t(1) << 32))
+    return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
   PR_TRY(g->colp.alloc(sizeof(int32_t) * (all.padded_len > 0 ? all.padded_len : 8)));
   PR_TRY(build_padded_cols(all, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
-  g->col.reset();
-  // class units launch at position k*C + x, so blockIdx % 8 == x: one XCD per class under the
-  // observed round-robin placement (any placement stays correct, only slower)
-  std::vector<Unit> order;
-  if (C > 1) {
-    size_t mx = 0;
-    for (auto &v : cls_units) mx = std::max(mx, v.size());
-    order.resize(mx * C, Unit{0, 0, 0, 0});
-    for (int x = 0; x < C; ++x)
-      for (size_t k = 0; k < mx; ++k)
-        order[k * C + x] = k < cls_units[x].size() ? cls_units[x][k] : Unit{0, 0, 0, x << 16};
+  // heavy wave units: LDS hot set per class, then the entry codes
+  {
+    const int slots = hot_slots_setting();
+    HotGeom hg{};
+    hg.P = P;
+    hg.Kp = C > 1 ? slots / P : 0;
+    hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
+    hg.S_pad = g->S_pad;
+    hg.Q_pad = g->Q_pad;
+    g->hot = hg;
+    int n_cu = 0;
+    PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
+    g->hot_grid = std::max(kClasses, n_cu / kClasses * kClasses);
+    PR_TRY(prepare_hot_kernel());
+    const size_t nu = wp.units.size();
+    g->n_hunits = (int64_t)nu;
+    PR_TRY(g->hunits.alloc(sizeof(Unit) * (nu + 1)));
+    PR_HIP(hipMemsetAsync(g->hunits.p, 0, sizeof(Unit) * (nu + 1), s));  // unit nu: the empty unit
+    PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kClasses + 1)));
+    PR_TRY(g->colh.alloc(sizeof(uint32_t) * (wp.len > 0 ? wp.len : 8)));
+    PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
+    PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kClasses + 1), hipMemcpyHostToDevice, s));
+    if (nu > 0) {
+      DevBuf dsrc_off, dcls, dlo;
+      PR_TRY(dsrc_off.alloc(sizeof(int64_t) * nu));
+      PR_TRY(dcls.alloc(sizeof(int32_t) * nu));
+      PR_TRY(dlo.alloc(sizeof(int64_t) * (C + 2)));
+      PR_HIP(hipMemcpyAsync(g->hunits.p, wp.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
+      PR_HIP(hipMemcpyAsync(dsrc_off.p, wp.src_off.data(), sizeof(int64_t) * nu, hipMemcpyHostToDevice, s));
+      PR_HIP(hipMemcpyAsync(dcls.p, wp.cls.data(), sizeof(int32_t) * nu, hipMemcpyHostToDevice, s));
+      PR_HIP(hipMemcpyAsync(dlo.p, hcls.data(), sizeof(int64_t) * (C + 2), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(256), 0, s, (int64_t)nu,
+                         kWaveUnit,
+                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dcls.as<int32_t>(), rp_all.as<int64_t>(), H,
+                         dlo.as<int64_t>(), g->col.as<int32_t>(), hg, g->colh.as<uint32_t>());
+      hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(kWave), 0, s, (int64_t)nu,
+                         g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
+      PR_HIP(hipGetLastError());
+      PR_HIP(hipStreamSynchronize(s));
+    }
   }
-  g->n_sunits = (int64_t)order.size();
+  rp_all.reset();
+  g->col.reset();
   g->n_units = (int64_t)light_units.size();
   g->n_long = (int64_t)lr_row.size();
   g->n_segs = (int64_t)seg_row.size();
   g->n_pieces = pieces;
   PR_TRY(g->units.alloc(sizeof(Unit) * (light_units.size() + 1)));
-  PR_TRY(g->sunits.alloc(sizeof(Unit) * (order.size() + 1)));
   PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (lr_row.size() + 1)));
   PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (lr_p0.size() + 1)));
   PR_TRY(g->seg_row.alloc(sizeof(int32_t) * (seg_row.size() + 1)));
@@ -585,8 +754,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
   if (!light_units.empty())
     PR_HIP(hipMemcpyAsync(g->units.p, light_units.data(), sizeof(Unit) * light_units.size(), hipMemcpyHostToDevice, s));
-  if (!order.empty())
-    PR_HIP(hipMemcpyAsync(g->sunits.p, order.data(), sizeof(Unit) * order.size(), hipMemcpyHostToDevice, s));
   if (!lr_row.empty())
     PR_HIP(hipMemcpyAsync(g->lr_row.p, lr_row.data(), sizeof(int32_t) * lr_row.size(), hipMemcpyHostToDevice, s));
   PR_HIP(hipMemcpyAsync(g->lr_p0.p, lr_p0.data(), sizeof(int32_t) * lr_p0.size(), hipMemcpyHostToDevice, s));

@@ -22,6 +22,8 @@
 // Only heavy rows (>= kHeavyMinIndeg in-links; a prefix of every region, since heavy vertices
 // sort first) are split: heavy row h has C partial slots partial[x][h] that an epilogue pass
 // adds in class order.  Light rows keep the fused single pass (pr_spmv.h k_spmv_units).
+// Heavy rows are processed as wave units whose entries address either the gather space or the
+// class's LDS hot set: the first Kp positions of every part's class-x region (pr_internal.h).
 //   cbuf    fp64[2][P*S_pad]  contributions r/d, double-buffered across iterations
 #pragma once
 
@@ -57,10 +59,14 @@ struct pr_graph {
 
   // part layout
   pr::DevBuf rowptr, col, colp, rowinfo, r;
-  pr::DevBuf lens, partial, sunits, seg_row, seg_cls, seg_p0;
+  // heavy rows (C > 1): wave units per class (hunits[hucum[x], hucum[x+1])), their entry codes,
+  // per-class partial sums partial[x][h], long segments (seg_*: pieces reduced in order)
+  pr::DevBuf colh, hmeta, hunits, hucum, partial, seg_row, seg_cls, seg_p0;
   int ep_blocks = 0;
   pr::ClassGeom geo{};
-  int64_t n_heavy = 0, n_sunits = 0, n_segs = 0;
+  pr::HotGeom hot{};
+  int hot_grid = 0;  // workgroups of k_spmv_hot (a multiple of 8: one per CU)
+  int64_t n_heavy = 0, n_hunits = 0, n_segs = 0;
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;
@@ -95,6 +101,8 @@ struct pr_graph {
 namespace pr {
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
+int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
+int launch_hot(pr_graph *g, int in_buf);  // the heavy-row pass (k_spmv_hot) on g's stream
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
 int group_exchange(pr_graph *const *parts, int n, int buf);

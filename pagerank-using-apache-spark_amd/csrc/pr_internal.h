@@ -104,6 +104,28 @@ constexpr uint32_t kRowHeavy = 1u << 31;   // class-split row (its sum comes fro
 // slots (write + read) and C row lengths, worth it only when enough gathers gain L2 locality.
 constexpr int kHeavyMinIndeg = 8;
 
+// ---- heavy rows: wave units with an LDS-resident hot set (pr_spmv.h k_spmv_hot) -------------
+// A wave unit is one wavefront's work: kWavePT in-link entries per lane, kWaveUnit entries in
+// all.  STREAM: whole (row, class) segments of consecutive heavy rows, every segment non-empty
+// (a row without class-x in-links gets one dummy entry that reads a zero); PIECE: kWaveUnit
+// entries of one long segment.  Entries are 32-bit codes:
+//   bit 31 set    kEntGlobal | byte offset of the contribution in the gather space (< 2 GiB)
+//   bit 31 clear  LDS byte address of a hot-set slot; slot 0 (address 0) holds 0.0
+// Padding and dummy entries are 0 -- also what a range-checked load past the unit returns.
+// Per unit and lane, one metadata word:
+//   bits 0-7   which of the lane's entries end a segment (STREAM)
+//   bits 8-13  the six partner-add predicates of the wave's segmented scan (pr_spmv.h)
+//   bits 14-23 segment index of the lane's first end within the unit
+constexpr int kWavePT = 8;
+constexpr int kWaveUnit = 64 * kWavePT;  // 512 (wave64)
+constexpr int kHotThreads = 1024;        // 16 waves per CU: one workgroup per CU
+constexpr uint32_t kEntGlobal = 1u << 31;
+constexpr uint32_t kEntZero = 0u;  // LDS slot 0
+constexpr uint32_t kMetaStep0 = 1u << 8;
+constexpr int kMetaExclShift = 14;
+// hot contributions kept in LDS per class (all parts together): 144 KiB of the CU's 160 KiB
+constexpr int kHotSlotsDefault = 18432;
+
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {
   int C;
@@ -114,6 +136,14 @@ struct ClassGeom {
     while (y + 1 < C && hcum[y + 1] <= h) ++y;
     return (int64_t)y * Q_pad + (h - hcum[y]);
   }
+};
+
+// Where a class's hot contributions live in the gather space: for every part p, positions
+// [p*S_pad + x*Q_pad, + q_load) go to LDS slots 1 + [p*Kp, p*Kp + q_load); slot 0 holds 0.0.
+struct HotGeom {
+  int P, Kp, q_load;
+  int64_t S_pad, Q_pad;
+  __host__ __device__ int slots() const { return P * Kp + 1; }
 };
 
 // Host plan over a part's row_ptr: units, their source offsets in the unpadded column array,

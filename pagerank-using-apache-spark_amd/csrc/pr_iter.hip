@@ -151,6 +151,23 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 
 }  // namespace
 
+int prepare_hot_kernel() {
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  return PR_OK;
+}
+
+int launch_hot(pr_graph *g, int in) {
+  const size_t lds = sizeof(double) * (size_t)g->hot.slots();
+  hipLaunchKernelGGL((k_spmv_hot<0, 0>), dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
+                     g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
+                     g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
+                     (uint32_t)(sizeof(double) * g->nparts * g->S_pad), g->partial.as<double>(),
+                     g->piece_part.as<double>(), g->n_heavy);
+  PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+
 int iter_reset(pr_graph *g, const double *init_host) {
   hipStream_t s = g->stream;
   DevBuf dinit;
@@ -201,11 +218,7 @@ int iter_compute(pr_graph *g) {
   int64_t n_parts = g->n_units;
   if (g->C > 1 && g->n_heavy > 0) {  // heavy rows: per-class sums, then the epilogue
     const int64_t H = g->n_heavy;
-    if (g->n_sunits > 0)
-      hipLaunchKernelGGL((k_spmv_split<kPerThread, true>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0, s,
-                         g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
-                         g->cbuf[in].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(), H,
-                         0xFFFFFFFFu);
+    if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_row.as<int32_t>(), g->seg_cls.as<int32_t>(), g->seg_p0.as<int32_t>(),

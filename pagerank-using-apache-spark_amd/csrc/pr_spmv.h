@@ -248,262 +248,187 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
 // ============================================================================================
 // Split layout (C column classes, pr_graph.h): per-class row sums, then one epilogue pass.
 // ============================================================================================
+// Heavy (row, class) segments are cut into wave units (pr_internal.h): one wavefront per unit,
+// no workgroup barriers.  k_spmv_hot runs one 1024-thread workgroup per CU (its LDS holds the
+// class's hot set, so only one fits); workgroup b serves class x = b % 8 -- under the observed
+// round-robin dispatch one XCD per class, so that XCD's L2 caches only class-x contributions --
+// and its 16 waves walk the class's unit list with a stride of (gridDim/8)*16 units.
+//
+// Per unit, lane l owns entries [8l, 8l + 8): two 16-byte buffer loads of entry codes (a wave
+// reads 2 KiB contiguous; lanes past the unit read 0 through the descriptor's range check) and
+// one 4-byte load of the lane's static metadata.  Each entry costs one LDS read (hot codes: the
+// most-gathered contributions, top out-degree first; every other lane reads slot 0 = 0.0) and
+// one buffer load of the gather space (hot codes turn into offsets >= 2^31: range-checked away,
+// no memory request), summed -- one of the two is an exact zero.  No branches, so the waits stay exact.
+// The loop is software-pipelined over a ring of three units: the codes of unit i+2 and the
+// values of unit i+1 are in flight while unit i is reduced.
+//
+// STREAM reduction: each lane sums its values along its segment ends; segments that cross lanes
+// are completed by a wave64 segmented scan in DPP (row_shr 1/2/4/8, row_bcast 15/31) whose
+// per-step "add the partner" predicates are static (a function of where the ends are) and come
+// precomputed in the metadata.  Segment s of the unit is row r0 + s, written to partial[x][row]
+// by buffer stores (lanes without an end at step j store out of range: no write).  PIECE: wave
+// sum.  Every sum has a fixed order: results are bitwise reproducible.
+typedef int pr_v2i __attribute__((ext_vector_type(2)));
 
-// Walk + segmented scan shared by both STREAM paths: every thread sums its PT values along the
-// unit's row boundaries (lrp in LDS); completed row sums land in rowsum[] (LDS).
-template <int PT>
-__device__ __forceinline__ void stream_row_sums(const double (&v)[PT], int n, int nr, const int32_t *lrp,
-                                                double *rowsum, int32_t *wrow_first, int32_t *wrow_last,
-                                                double *wval_last) {
-  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
-  const int i0 = t * PT;
-  int carry_row = -1, first_row = -1;
-  double carry_val = 0.0, first_sum = 0.0;
-  if (i0 < n) {
-    int lo = 0, hi = nr + 1;  // first k with lrp[k] > i0
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (lrp[mid] <= i0) lo = mid + 1;
-      else hi = mid;
-    }
-    int cur = lo - 1;
-    const int kstart = cur;
-    const bool started_before = lrp[cur] < i0;
-    int next_end = lrp[cur + 1];
-    double acc = 0.0;
-    bool open = false;
-#pragma unroll
-    for (int j = 0; j < PT; ++j) {
-      if (i0 + j < n) {
-        acc = __dadd_rn(acc, v[j]);
-        open = true;
-        if (i0 + j + 1 == next_end) {
-          if (cur == kstart && started_before) {
-            first_row = cur;
-            first_sum = acc;
-          } else {
-            rowsum[cur] = acc;
-          }
-          acc = 0.0;
-          open = false;
-          ++cur;
-          while (cur < nr && lrp[cur + 1] == lrp[cur]) ++cur;
-          next_end = (cur < nr) ? lrp[cur + 1] : INT_MAX;
-        }
-      }
-    }
-    if (open) {
-      carry_row = cur;
-      carry_val = acc;
-    }
-  }
-  int srow = carry_row;
-  double sval = carry_val;
-#pragma unroll
-  for (int off = 1; off < kWave; off <<= 1) {
-    const int prow = __shfl_up(srow, off, kWave);
-    const double pval = __shfl_up(sval, off, kWave);
-    if (lane >= off && srow >= 0 && prow == srow) sval = __dadd_rn(pval, sval);
-  }
-  const int lane0_row = __shfl(carry_row, 0, kWave);
-  if (lane == kWave - 1) {
-    wrow_last[w] = srow;
-    wval_last[w] = sval;
-    wrow_first[w] = lane0_row;
-  }
-  __syncthreads();
-  int prow_in = -1;
-  double pval_in = 0.0;
-  for (int ww = 0; ww < w; ++ww) {
-    const int rl = wrow_last[ww];
-    const bool full = (rl >= 0) && (wrow_first[ww] == rl);
-    if (full && prow_in == rl) {
-      pval_in = __dadd_rn(pval_in, wval_last[ww]);
-    } else {
-      prow_in = rl;
-      pval_in = (rl >= 0) ? wval_last[ww] : 0.0;
-    }
-  }
-  if (srow >= 0 && srow == prow_in && lane0_row == srow) sval = __dadd_rn(pval_in, sval);
-  int erow = __shfl_up(srow, 1, kWave);
-  double eval = __shfl_up(sval, 1, kWave);
-  if (lane == 0) {
-    erow = prow_in;
-    eval = pval_in;
-  }
-  if (first_row >= 0) rowsum[first_row] = (erow == first_row) ? __dadd_rn(eval, first_sum) : first_sum;
-  __syncthreads();
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const pr_v2i v = __builtin_bit_cast(pr_v2i, x);
+  pr_v2i r;
+  r.x = __builtin_amdgcn_update_dpp(0, v.x, CTRL, 0xF, 0xF, true);
+  r.y = __builtin_amdgcn_update_dpp(0, v.y, CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, r);
 }
 
-// Class-x work unit (launched at blockIdx % 8 == x): gathers only class-x contributions and
-// writes partial[x][row] for every row of the unit (0 for rows without class-x in-links).
-template <int PT, bool NT, bool MASK_GATHER = false>
-__global__ __launch_bounds__(kThreads) void k_spmv_split(
-    const Unit *__restrict__ units, const uint16_t *__restrict__ lens, const int32_t *__restrict__ colp,
-    const double *__restrict__ cin, double *__restrict__ partial, double *__restrict__ piece_part,
-    int64_t R, uint32_t gather_mask = 0xFFFFFFFFu) {
-  static_assert(kUnitRows <= 4 * kThreads, "lens scan covers 4 rows per thread");
-  __shared__ double rowsum[kUnitRows];
-  __shared__ int32_t lrp[kUnitRows + 1];
-  __shared__ double red[kThreads / kWave];
-  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
-  __shared__ double wval_last[kThreads / kWave];
-  __shared__ uint32_t scan_scratch[kThreads / kWave];
+struct WaveCodes {
+  uint32_t c[kWavePT];
+  uint32_t meta;
+};
 
-  const int t = threadIdx.x;
-  const Unit u = units[blockIdx.x];
-  const int n = unit_n(u), x = unit_cls(u);
-  if (u.meta == 0) return;  // empty padding unit (or a unit of zero rows)
-  const int i0 = t * PT;
-  const bool stream = u.meta > 0;
-  const int nr = stream ? u.meta : 0;
-  const int32_t r0 = u.r0;
+__device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *__restrict__ colh,
+                                                const uint32_t *__restrict__ hmeta, int64_t k, WaveCodes &w) {
+  // per-unit descriptor: base and size are wave-uniform (u lives in SGPRs)
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(colh + (int64_t)u.p8 * 8), 0, u.n * 4, 0x00020000);
+  const int base = lane_id() * kWavePT * 4;
+#pragma unroll
+  for (int q = 0; q < kWavePT / 4; ++q) {
+    const pr_v4i x = __builtin_bit_cast(pr_v4i, __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16 * q, 0, 2));
+    w.c[4 * q + 0] = (uint32_t)x.x;
+    w.c[4 * q + 1] = (uint32_t)x.y;
+    w.c[4 * q + 2] = (uint32_t)x.z;
+    w.c[4 * q + 3] = (uint32_t)x.w;
+  }
+  const __amdgpu_buffer_rsrc_t ms =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(hmeta + k * kWave), 0, u.n > 0 ? kWave * 4 : 0, 0x00020000);
+  w.meta = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ms, lane_id() * 4, 0, 2);
+}
 
-  int32_t ci[PT];
-  if (i0 < n) {
-    load_cols<PT, NT>(colp + (int64_t)u.p8 * 8 + i0, ci);
-  } else {
+// DIAG (diagnostics library only; results wrong when != 0): 1 = every value from LDS (no
+// gather-space loads), 2 = no partial stores, 3 = non-temporal partial stores.
+template <int DIAG>
+__device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, __amdgpu_buffer_rsrc_t crs,
+                                                 double (&v)[kWavePT]) {
 #pragma unroll
-    for (int j = 0; j < PT; ++j) ci[j] = 0;
+  for (int j = 0; j < kWavePT; ++j) {
+    const uint32_t c = w.c[j];
+    const bool glob = (int32_t)c < 0;
+    uint32_t la = glob ? 0u : c;
+    if constexpr (DIAG == 1) la = c & 0xFFF8u;
+    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    double b = 0.0;
+    if constexpr (DIAG != 1)  // LDS codes become offsets >= 2^31: out of range, no request
+      b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, c ^ kEntGlobal, 0, 0));
+    v[j] = __dadd_rn(a, b);
   }
-  uint32_t l4[4] = {0, 0, 0, 0};
-  if (stream) {  // streamed once per iteration: non-temporal, keep the L2 for contributions
-    const uint16_t *lx = lens + (int64_t)x * (R + 1) + r0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * t + q < nr) l4[q] = __builtin_nontemporal_load(lx + 4 * t + q);
-  }
-  double v[PT];
-#pragma unroll
-  for (int j = 0; j < PT; ++j) {
-    int32_t c = ci[j];
-    if constexpr (MASK_GATHER) c = (int32_t)((uint32_t)c & gather_mask);  // diagnostics only
-    v[j] = (i0 + j < n) ? cin[c] : 0.0;
-  }
+}
 
-  if (!stream) {  // PIECE of a long (row, class) segment
+template <int DIAG>
+__device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
+                                                 __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part) {
+  if (u.meta < 0) {  // PIECE of a long segment
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < PT; ++j) acc = __dadd_rn(acc, v[j]);
-    acc = block_sum<kThreads>(acc, red);
-    if (t == 0) piece_part[-u.meta - 1] = acc;
+    for (int j = 0; j < kWavePT; ++j) acc = __dadd_rn(acc, v[j]);
+    acc = wave_sum(acc);
+    if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
-
-  // unit-local row pointers from the class's uint16 row lengths
-  uint32_t tot;
-  const uint32_t base = block_exclusive_scan<kThreads>(l4[0] + l4[1] + l4[2] + l4[3], scan_scratch, &tot);
-  {
-    uint32_t acc = base;
+  const uint32_t endm = w.meta & 0xFFu;
+  double sv[kWavePT];
+  double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (4 * t + q < nr) lrp[4 * t + q] = (int32_t)acc;
-      acc += l4[q];
-    }
-    if (t == 0) lrp[nr] = (int32_t)tot;
+  for (int j = 0; j < kWavePT; ++j) {
+    acc = __dadd_rn(acc, v[j]);
+    sv[j] = acc;
+    if (endm & (1u << j)) acc = 0.0;
   }
-  __syncthreads();
-  stream_row_sums<PT>(v, n, nr, lrp, rowsum, wrow_first, wrow_last, wval_last);
-  double *px = partial + (int64_t)x * R + r0;
-  for (int k = t; k < nr; k += kThreads)
-    __builtin_nontemporal_store((lrp[k + 1] > lrp[k]) ? rowsum[k] : 0.0, px + k);
+  // segmented inclusive scan of the lane tails; partner-add predicates precomputed
+  double a = acc, p;
+  p = dpp_f64<0x111>(a);  // row_shr:1
+  if (w.meta & kMetaStep0) a = __dadd_rn(p, a);
+  p = dpp_f64<0x112>(a);  // row_shr:2
+  if (w.meta & (kMetaStep0 << 1)) a = __dadd_rn(p, a);
+  p = dpp_f64<0x114>(a);  // row_shr:4
+  if (w.meta & (kMetaStep0 << 2)) a = __dadd_rn(p, a);
+  p = dpp_f64<0x118>(a);  // row_shr:8
+  if (w.meta & (kMetaStep0 << 3)) a = __dadd_rn(p, a);
+  p = dpp_f64<0x142>(a);  // row_bcast:15
+  if (w.meta & (kMetaStep0 << 4)) a = __dadd_rn(p, a);
+  p = dpp_f64<0x143>(a);  // row_bcast:31
+  if (w.meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
+  const double carry = dpp_f64<0x138>(a);  // wave_shr:1 (lane 0 reads 0)
+  // lane's first segment end gets the carry; ends are rows r0 + excl, r0 + excl + 1, ...
+  uint32_t off = (uint32_t)(u.r0 + (int)(w.meta >> kMetaExclShift)) * 8u;
+  bool first = true;
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) {
+    const bool e = (endm >> j) & 1u;
+    const double sj = (e && first) ? __dadd_rn(carry, sv[j]) : sv[j];
+    first = first && !e;
+    if constexpr (DIAG != 2) {
+      const uint32_t o = e ? off : 0xFFFFFFF0u;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, sj), prs, o, 0, DIAG == 3 ? 2 : 0);
+    }
+    off += e ? 8u : 0u;
+  }
 }
 
-// Persistent form of k_spmv_split: gridDim (a multiple of 8) workgroups walk the unit list with
-// stride gridDim, so unit k still runs at blockIdx % 8 == k % 8 (its class's XCD).  While one
-// unit is reduced, the next unit's gather positions are already in flight (descriptor two units
-// ahead), hiding the HBM latency that bounds a one-unit-per-workgroup launch.
-template <int PT, bool NT>
-__device__ __forceinline__ void split_unit(const Unit &u, const int32_t (&ci)[PT], const uint16_t *__restrict__ lens,
-                                           const double *__restrict__ cin, double *__restrict__ partial,
-                                           double *__restrict__ piece_part, int64_t R, double *rowsum,
-                                           int32_t *lrp, double *red, int32_t *wrow_first, int32_t *wrow_last,
-                                           double *wval_last, uint32_t *scan_scratch) {
-  const int t = threadIdx.x;
-  const int n = unit_n(u), x = unit_cls(u);
-  const int i0 = t * PT;
-  const bool stream = u.meta > 0;
-  const int nr = stream ? u.meta : 0;
-  const int32_t r0 = u.r0;
-  uint32_t l4[4] = {0, 0, 0, 0};
-  if (stream) {
-    const uint16_t *lx = lens + (int64_t)x * (R + 1) + r0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (4 * t + q < nr) l4[q] = __builtin_nontemporal_load(lx + 4 * t + q);
+template <int DEPTH_UNUSED = 0, int DIAG = 0>
+__global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
+                                                          const int64_t *__restrict__ ucum, HotGeom hg,
+                                                          const uint32_t *__restrict__ colh,
+                                                          const uint32_t *__restrict__ hmeta,
+                                                          const double *__restrict__ cin, uint32_t cin_bytes,
+                                                          double *__restrict__ partial,
+                                                          double *__restrict__ piece_part, int64_t H) {
+  extern __shared__ double hot[];
+  const int x = (int)(blockIdx.x % kClasses);
+  const int team = (int)(blockIdx.x / kClasses), nteams = (int)(gridDim.x / kClasses);
+  // stage the class's hot contributions (the previous iteration's, final before this launch)
+  const int nh = hg.P * hg.Kp;
+  for (int i = threadIdx.x; i < nh; i += kHotThreads) {
+    const int p = i / hg.Kp, q = i - p * hg.Kp;
+    hot[1 + i] = q < hg.q_load ? cin[(int64_t)p * hg.S_pad + (int64_t)x * hg.Q_pad + q] : 0.0;
   }
-  double v[PT];
-#pragma unroll
-  for (int j = 0; j < PT; ++j) v[j] = (i0 + j < n) ? cin[ci[j]] : 0.0;
-  if (!stream) {
-    double acc = 0.0;
-#pragma unroll
-    for (int j = 0; j < PT; ++j) acc = __dadd_rn(acc, v[j]);
-    acc = block_sum<kThreads>(acc, red);
-    if (t == 0) piece_part[-u.meta - 1] = acc;
-    return;
-  }
-  uint32_t tot;
-  const uint32_t base = block_exclusive_scan<kThreads>(l4[0] + l4[1] + l4[2] + l4[3], scan_scratch, &tot);
-  {
-    uint32_t acc = base;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (4 * t + q < nr) lrp[4 * t + q] = (int32_t)acc;
-      acc += l4[q];
-    }
-    if (t == 0) lrp[nr] = (int32_t)tot;
-  }
+  if (threadIdx.x == 0) hot[0] = 0.0;
   __syncthreads();
-  stream_row_sums<PT>(v, n, nr, lrp, rowsum, wrow_first, wrow_last, wval_last);
-  double *px = partial + (int64_t)x * R + r0;
-  for (int k = t; k < nr; k += kThreads)
-    __builtin_nontemporal_store((lrp[k + 1] > lrp[k]) ? rowsum[k] : 0.0, px + k);
-  __syncthreads();  // rowsum / lrp are reused by the next unit
-}
-
-template <int PT, bool NT, int MINW = 1>
-__global__ __launch_bounds__(kThreads, MINW) void k_spmv_split_persist(
-    const Unit *__restrict__ units, int64_t n_units, const uint16_t *__restrict__ lens,
-    const int32_t *__restrict__ colp, const double *__restrict__ cin, double *__restrict__ partial,
-    double *__restrict__ piece_part, int64_t R) {
-  __shared__ double rowsum[kUnitRows];
-  __shared__ int32_t lrp[kUnitRows + 1];
-  __shared__ double red[kThreads / kWave];
-  __shared__ int32_t wrow_first[kThreads / kWave], wrow_last[kThreads / kWave];
-  __shared__ double wval_last[kThreads / kWave];
-  __shared__ uint32_t scan_scratch[kThreads / kWave];
-  const int64_t stride = gridDim.x;
-  int64_t k = blockIdx.x;
-  if (k >= n_units) return;
-  const int i0 = threadIdx.x * PT;
-  const Unit empty{0, 0, 0, 0};
-  Unit u = units[k];
-  Unit un = (k + stride < n_units) ? units[k + stride] : empty;
-  int32_t ci[PT];
-  if (i0 < unit_n(u)) load_cols<PT, NT>(colp + (int64_t)u.p8 * 8 + i0, ci);
-  else {
-#pragma unroll
-    for (int j = 0; j < PT; ++j) ci[j] = 0;
-  }
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(partial + (int64_t)x * H), 0, (uint32_t)(H * 8), 0x00020000);
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  const int64_t beg = ucum[x], end = ucum[x + 1];
+  const int64_t stride = (int64_t)nteams * (kHotThreads / kWave);
+  int64_t k = beg + (int64_t)team * (kHotThreads / kWave) + wv;
+  if (k >= end) return;
+  // unit descriptors through the scalar cache; index n_units (= ucum[kClasses]) is an empty unit
+  const __attribute__((address_space(4))) pr_v4i *cu = (const __attribute__((address_space(4))) pr_v4i *)units;
+  auto unit_at = [&](int64_t i) -> Unit {
+    const pr_v4i q = cu[i];
+    return Unit{(uint32_t)q.x, q.y, q.z, q.w};
+  };
+  const int64_t none_k = ucum[kClasses];
+  // ring of three units: codes of i+2 and values of i+1 in flight while unit i is reduced
+  Unit u[3];
+  WaveCodes wc[3];
+  double v[3][kWavePT];
+  u[0] = unit_at(k);
+  wave_unit_codes(u[0], colh, hmeta, k, wc[0]);
+  u[1] = unit_at((k + stride < end) ? k + stride : none_k);
+  wave_unit_codes(u[1], colh, hmeta, k + stride, wc[1]);
+  wave_unit_gather<DIAG>(wc[0], hot, crs, v[0]);
   while (true) {
-    const int64_t k1 = k + stride, k2 = k1 + stride;
-    int32_t ci1[PT];
-    if (k1 < n_units && i0 < unit_n(un)) load_cols<PT, NT>(colp + (int64_t)un.p8 * 8 + i0, ci1);
-    else {
 #pragma unroll
-      for (int j = 0; j < PT; ++j) ci1[j] = 0;
+    for (int sl = 0; sl < 3; ++sl) {
+      const int s1 = (sl + 1) % 3, s2 = (sl + 2) % 3;
+      const int64_t k2 = k + 2 * stride;
+      u[s2] = unit_at(k2 < end ? k2 : none_k);
+      wave_unit_codes(u[s2], colh, hmeta, k2, wc[s2]);
+      wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
+      wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part);
+      k += stride;
+      if (k >= end) return;
     }
-    const Unit unn = (k2 < n_units) ? units[k2] : empty;
-    if (u.meta != 0)
-      split_unit<PT, NT>(u, ci, lens, cin, partial, piece_part, R, rowsum, lrp, red, wrow_first, wrow_last,
-                         wval_last, scan_scratch);
-    if (k1 >= n_units) break;
-    u = un;
-    un = unn;
-#pragma unroll
-    for (int j = 0; j < PT; ++j) ci[j] = ci1[j];
-    k = k1;
   }
 }
 

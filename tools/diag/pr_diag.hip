@@ -72,6 +72,28 @@ void launch(pr_graph *g, Layout *L, uint32_t mask) {
 
 }  // namespace
 
+
+// ---- gather microbenchmark (diagnostics): uniform random 8-byte loads from a table ----------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+template <int AUX>
+__global__ __launch_bounds__(256) void k_gather_bench(const double *__restrict__ table, uint32_t n_words,
+                                                      int64_t n_threads, uint32_t seed, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_threads) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, n_words * 8u, 0x00020000);
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t w = mix32((uint32_t)t * 8u + j + seed) % n_words;
+    acc += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, w * 8u, 0, AUX));
+  }
+  if (acc == 12345.0) out[t] = acc;
+}
+
 extern "C" {
 
 // variant: 0 = PT 8 + nt cols (product), 1 = PT 8 plain cols, 2 = PT 16 + nt, 3 = PT 4 + nt,
@@ -120,37 +142,36 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
   return PR_OK;
 }
 
-// Split layout variants on the graph's own layout: 0 = product kernel, 1 = gathers masked by
-// `mask` (diagnostics: results wrong).
+// Split layout: time the heavy-row kernel k_spmv_hot<0, DIAG> on the graph's own layout.
+// variant = DIAG: 0 = product, 1 = all values from LDS, 2 = no partial stores, 3 = non-temporal
+// partial stores (1, 2: diagnostics, results wrong).  The hot-set size is a build setting
+// (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
+  (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
+  static const void *tab[4] = {reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 3>)};
+  if (variant < 0 || variant > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
+  const void *kern = tab[variant];
+  PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  const uint32_t cin_bytes = (uint32_t)(sizeof(double) * g->nparts * g->S_pad);
+  Unit *units = g->hunits.as<Unit>();
+  int64_t *ucum = g->hucum.as<int64_t>();
+  HotGeom hg = g->hot;
+  uint32_t *colh = g->colh.as<uint32_t>(), *hmeta = g->hmeta.as<uint32_t>();
+  double *cin = g->cbuf[0].as<double>(), *partial = g->partial.as<double>(), *pp = g->piece_part.as<double>();
+  int64_t H = g->n_heavy;
+  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &pp, &H};
   hipEvent_t a, b;
   PR_HIP(hipEventCreate(&a));
   PR_HIP(hipEventCreate(&b));
   PR_HIP(hipEventRecord(a, g->stream));
-  for (int i = 0; i < iters; ++i) {
-    if (variant == 4)
-      hipLaunchKernelGGL((k_spmv_split_persist<kPerThread, true, 8>), dim3(2048), dim3(kThreads), 0,
-                         g->stream, g->sunits.as<Unit>(), g->n_sunits, g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
-                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
-                         g->n_heavy);
-    else if (variant == 2 || variant == 3)
-      hipLaunchKernelGGL((k_spmv_split_persist<kPerThread, true>), dim3(variant == 2 ? 1536 : 1024), dim3(kThreads), 0,
-                         g->stream, g->sunits.as<Unit>(), g->n_sunits, g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
-                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
-                         g->n_heavy);
-    else if (variant == 0)
-      hipLaunchKernelGGL((k_spmv_split<kPerThread, true, false>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0,
-                         g->stream, g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
-                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
-                         g->n_heavy, mask);
-    else
-      hipLaunchKernelGGL((k_spmv_split<kPerThread, true, true>), dim3((unsigned)g->n_sunits), dim3(kThreads), 0,
-                         g->stream, g->sunits.as<Unit>(), g->lens.as<uint16_t>(), g->colp.as<int32_t>(),
-                         g->cbuf[0].as<double>(), g->partial.as<double>(), g->piece_part.as<double>(),
-                         g->n_heavy, mask);
-  }
+  for (int i = 0; i < iters; ++i)
+    PR_HIP(hipLaunchKernel(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), args,
+                           sizeof(double) * (size_t)g->hot.slots(), g->stream));
   PR_HIP(hipGetLastError());
   PR_HIP(hipEventRecord(b, g->stream));
   PR_HIP(hipEventSynchronize(b));
@@ -159,6 +180,48 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   *ms_out = ms / iters;
+  return PR_OK;
+}
+
+
+// mode: 0 hipMalloc + plain loads, 1 nt, 2 sc1, 3 sc0|sc1, 4 uncached memory (hipDeviceMallocUncached),
+// 5 fine-grained memory (hipDeviceMallocFinegrained).  8 loads per thread.
+int prd_gather_bench(int device, int64_t table_bytes, int64_t n_loads, int mode, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  void *tab = nullptr, *out = nullptr;
+  const unsigned flags = mode == 4 ? hipDeviceMallocUncached : (mode == 5 ? hipDeviceMallocFinegrained : 0u);
+  if (flags) PR_HIP(hipExtMallocWithFlags(&tab, (size_t)table_bytes, flags));
+  else PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8));
+  const int64_t nt = n_loads / 8;
+  const uint32_t nw = (uint32_t)(table_bytes / 8);
+  const dim3 grid((unsigned)((nt + 255) / 256));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {  // rep 0 warms
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i) {
+      const uint32_t seed = 977u * (uint32_t)i;
+      switch (mode) {
+        case 1: hipLaunchKernelGGL(k_gather_bench<2>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
+        case 2: hipLaunchKernelGGL(k_gather_bench<16>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
+        case 3: hipLaunchKernelGGL(k_gather_bench<17>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
+        default: hipLaunchKernelGGL(k_gather_bench<0>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
+      }
+    }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
   return PR_OK;
 }
 
