@@ -455,8 +455,7 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 static int hot_slots_setting() {
   int k = kHotSlotsDefault;
   if (const char *e = getenv("PR_HOT_SLOTS")) k = atoi(e);  // tuning knob
-  const int max_slots = (160 * 1024) / 8 - 64;
-  return std::max(0, std::min(k, max_slots));
+  return std::max(0, std::min(k, kHotSlotsMax));
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {

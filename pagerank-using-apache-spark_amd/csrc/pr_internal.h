@@ -123,8 +123,12 @@ constexpr uint32_t kEntGlobal = 1u << 31;
 constexpr uint32_t kEntZero = 0u;  // LDS slot 0
 constexpr uint32_t kMetaStep0 = 1u << 8;
 constexpr int kMetaExclShift = 14;
-// hot contributions kept in LDS per class (all parts together): 144 KiB of the CU's 160 KiB
-constexpr int kHotSlotsDefault = 18432;
+// LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part),
+// then one staging window of kStageSlots segment sums per wave (32 KiB in all).
+constexpr int kStageSlots = 256;
+constexpr int kHotLdsBytes = 160 * 1024;
+constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 2;
+constexpr int kHotSlotsDefault = kHotSlotsMax;  // 16382 hot contributions (128 KiB)
 
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {
@@ -144,6 +148,10 @@ struct HotGeom {
   int P, Kp, q_load;
   int64_t S_pad, Q_pad;
   __host__ __device__ int slots() const { return P * Kp + 1; }
+  __host__ __device__ int stage_off() const { return (slots() + 1) & ~1; }  // 16-byte aligned
+  __host__ __device__ size_t lds_bytes() const {
+    return sizeof(double) * ((size_t)stage_off() + (size_t)(kHotThreads / 64) * kStageSlots);
+  }
 };
 
 // Host plan over a part's row_ptr: units, their source offsets in the unpadded column array,

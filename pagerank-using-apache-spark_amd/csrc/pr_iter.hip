@@ -158,7 +158,7 @@ int prepare_hot_kernel() {
 }
 
 int launch_hot(pr_graph *g, int in) {
-  const size_t lds = sizeof(double) * (size_t)g->hot.slots();
+  const size_t lds = g->hot.lds_bytes();
   hipLaunchKernelGGL((k_spmv_hot<0, 0>), dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
                      g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),

@@ -267,8 +267,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
 // are completed by a wave64 segmented scan in DPP (row_shr 1/2/4/8, row_bcast 15/31) whose
 // per-step "add the partner" predicates are static (a function of where the ends are) and come
 // precomputed in the metadata.  Segment s of the unit is row r0 + s, written to partial[x][row]
-// by buffer stores (lanes without an end at step j store out of range: no write).  PIECE: wave
-// sum.  Every sum has a fixed order: results are bitwise reproducible.
+// through the wave's LDS staging window as coalesced stores.  PIECE: wave sum.  Every sum has a fixed order: results are bitwise reproducible.
 typedef int pr_v2i __attribute__((ext_vector_type(2)));
 
 template <int CTRL>
@@ -305,7 +304,9 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *_
 }
 
 // DIAG (diagnostics library only; results wrong when != 0): 1 = every value from LDS (no
-// gather-space loads), 2 = no partial stores, 3 = non-temporal partial stores.
+// gather-space loads), 2 = no partial stores, 3 = non-temporal partial stores, 4 / 5 = every
+// gather-space load folded into the first 4 / 32 MiB (L2- / Infinity-Cache-resident), 6 =
+// exec-masked gathers, 8 = every gather instruction reads 512 contiguous bytes.
 template <int DIAG>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, __amdgpu_buffer_rsrc_t crs,
                                                  double (&v)[kWavePT]) {
@@ -317,15 +318,26 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
     if constexpr (DIAG == 1) la = c & 0xFFF8u;
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
     double b = 0.0;
-    if constexpr (DIAG != 1)  // LDS codes become offsets >= 2^31: out of range, no request
-      b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, c ^ kEntGlobal, 0, 0));
+    uint32_t go = c ^ kEntGlobal;  // LDS codes become offsets >= 2^31: out of range, no request
+    if constexpr (DIAG == 4) go = glob ? (go & 0x3FFFF8u) : go;   // every gather within 4 MiB
+    if constexpr (DIAG == 5) go = glob ? (go & 0x1FFFFF8u) : go;  // every gather within 32 MiB
+    if constexpr (DIAG == 8)  // every wave-instruction reads 512 contiguous bytes
+      go = glob ? ((__builtin_amdgcn_readfirstlane(go) & 0x3FF000u) + (uint32_t)lane_id() * 8u) : go;
+    if constexpr (DIAG == 6) {  // exec-masked instead of range-checked
+      if (glob) b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, go, 0, 0));
+    } else if constexpr (DIAG != 1) {
+      // DIAG 9..12: cache-policy bits of the gather (nt, sc1, sc0|sc1, sc0)
+      constexpr int AUX = DIAG == 9 ? 2 : (DIAG == 10 ? 16 : (DIAG == 11 ? 17 : (DIAG == 12 ? 1 : 0)));
+      b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, go, 0, AUX));
+    }
     v[j] = __dadd_rn(a, b);
   }
 }
 
 template <int DIAG>
 __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
-                                                 __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part) {
+                                                 __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
+                                                 double *stage) {
   if (u.meta < 0) {  // PIECE of a long segment
     double acc = 0.0;
 #pragma unroll
@@ -358,19 +370,26 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   p = dpp_f64<0x143>(a);  // row_bcast:31
   if (w.meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
   const double carry = dpp_f64<0x138>(a);  // wave_shr:1 (lane 0 reads 0)
-  // lane's first segment end gets the carry; ends are rows r0 + excl, r0 + excl + 1, ...
-  uint32_t off = (uint32_t)(u.r0 + (int)(w.meta >> kMetaExclShift)) * 8u;
-  bool first = true;
+  // lane's first segment end gets the carry; segment s of the unit is row r0 + s.  The sums are
+  // staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced 512-byte
+  // stores instead of eight scattered store instructions.
+  const int e0 = (int)(w.meta >> kMetaExclShift), nseg = u.meta;
+  for (int base = 0; base < nseg; base += kStageSlots) {
+    int e = e0 - base;
+    bool first = true;
 #pragma unroll
-  for (int j = 0; j < kWavePT; ++j) {
-    const bool e = (endm >> j) & 1u;
-    const double sj = (e && first) ? __dadd_rn(carry, sv[j]) : sv[j];
-    first = first && !e;
-    if constexpr (DIAG != 2) {
-      const uint32_t o = e ? off : 0xFFFFFFF0u;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, sj), prs, o, 0, DIAG == 3 ? 2 : 0);
+    for (int j = 0; j < kWavePT; ++j) {
+      const bool end = (endm >> j) & 1u;
+      if (end && e >= 0 && e < kStageSlots) stage[e] = first ? __dadd_rn(carry, sv[j]) : sv[j];
+      if (end) first = false;
+      e += end ? 1 : 0;
     }
-    off += e ? 8u : 0u;
+    const int n = min(kStageSlots, nseg - base);
+    for (int i = lane_id(); i < n; i += kWave) {
+      const uint32_t o = (uint32_t)(u.r0 + base + i) * 8u;
+      if constexpr (DIAG != 2)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i]), prs, o, 0, DIAG == 3 ? 2 : 0);
+    }
   }
 }
 
@@ -397,6 +416,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)(partial + (int64_t)x * H), 0, (uint32_t)(H * 8), 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int64_t beg = ucum[x], end = ucum[x + 1];
   const int64_t stride = (int64_t)nteams * (kHotThreads / kWave);
   int64_t k = beg + (int64_t)team * (kHotThreads / kWave) + wv;
@@ -425,7 +445,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
       u[s2] = unit_at(k2 < end ? k2 : none_k);
       wave_unit_codes(u[s2], colh, hmeta, k2, wc[s2]);
       wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
-      wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part);
+      wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
       k += stride;
       if (k >= end) return;
     }

@@ -144,16 +144,25 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 
 // Split layout: time the heavy-row kernel k_spmv_hot<0, DIAG> on the graph's own layout.
 // variant = DIAG: 0 = product, 1 = all values from LDS, 2 = no partial stores, 3 = non-temporal
-// partial stores (1, 2: diagnostics, results wrong).  The hot-set size is a build setting
+// partial stores, 4 / 5 = gathers folded into 4 / 32 MiB (1, 2, 4, 5: diagnostics, results wrong).  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[4] = {reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[13] = {reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 3>)};
-  if (variant < 0 || variant > 3) return fail(PR_ERR_INVALID, "unknown variant");
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 4>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 5>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 6>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 8>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 9>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 10>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 11>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 12>)};
+  if (variant < 0 || variant > 12 || variant == 7) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -171,7 +180,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   PR_HIP(hipEventRecord(a, g->stream));
   for (int i = 0; i < iters; ++i)
     PR_HIP(hipLaunchKernel(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), args,
-                           sizeof(double) * (size_t)g->hot.slots(), g->stream));
+                           g->hot.lds_bytes(), g->stream));
   PR_HIP(hipGetLastError());
   PR_HIP(hipEventRecord(b, g->stream));
   PR_HIP(hipEventSynchronize(b));

@@ -13,8 +13,8 @@ import os
 import sys
 
 # the SpMV pass of one iteration = these kernels (pr_iter.hip iter_compute)
-PASS_KERNELS = ("k_spmv_units", "k_spmv_split", "k_seg_reduce", "k_epilogue")
-KERNEL = "k_spmv_"
+PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue", "k_finalize")
+KERNEL = "k_spmv_hot"
 
 
 def rows(pattern):
