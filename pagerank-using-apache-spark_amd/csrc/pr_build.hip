@@ -115,13 +115,13 @@ __global__ void k_vflags(int32_t V, const uint8_t *__restrict__ is_key,
 
 // Internal order key: heavy before light (split layout only), then out-degree descending,
 // original ID ascending.  *n_light counts the light vertices.
-__global__ void k_order_keys(int32_t V, int b, int bd, uint64_t maxd, bool split,
+__global__ void k_order_keys(int32_t V, int b, int bd, uint64_t maxd, bool split, int heavy_min,
                              const int32_t *__restrict__ deg, const int64_t *__restrict__ rowptr,
                              uint64_t *__restrict__ vk, unsigned long long *__restrict__ n_light) {
   unsigned long long nl = 0;
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
        v += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t light = (split && rowptr[v + 1] - rowptr[v] < kHeavyMinIndeg) ? 1ull : 0ull;
+    const uint64_t light = (split && rowptr[v + 1] - rowptr[v] < heavy_min) ? 1ull : 0ull;
     nl += light;
     vk[v] = (light << (b + bd)) | ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
   }
@@ -452,6 +452,20 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
   }
 }
 
+// Tuning knobs read at build time: column classes of the split layout (8 = one
+// per XCD, 16 = two per XCD) and the in-degree from which a row is class-split.
+static int class_setting() {
+  int c = kMaxClasses;
+  if (const char *e = getenv("PR_CLASSES")) c = atoi(e);
+  return c == 16 ? 16 : 8;
+}
+
+static int heavy_min_setting() {
+  int h = kHeavyMinIndeg;
+  if (const char *e = getenv("PR_HEAVY_MIN")) h = atoi(e);
+  return std::max(1, h);
+}
+
 static int hot_slots_setting() {
   int k = kHotSlotsDefault;
   if (const char *e = getenv("PR_HOT_SLOTS")) k = atoi(e);  // tuning knob
@@ -459,7 +473,7 @@ static int hot_slots_setting() {
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
-  static_assert(kClasses >= 1 && kClasses <= 16, "class count");
+  static_assert(kMaxClasses == 2 * kXcds && kClasses == kXcds, "class counts");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -551,9 +565,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   g->n_local = V > part ? (V - part + P - 1) / P : 0;
   if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
   // Column classes: one per XCD when the part's contribution slice outgrows the L2s (pr_graph.h).
-  int C = (g->n_local_max * 8 > kSplitMinSliceBytes) ? kClasses : 1;
+  const int c_split = class_setting();
+  int C = (g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
-  if (g->flags & PR_LAYOUT_SPLIT) C = kClasses;
+  if (g->flags & PR_LAYOUT_SPLIT) C = c_split;
   // heavy-row entry codes are byte offsets below 2^31 (pr_internal.h)
   if ((int64_t)P * (g->n_local_max + 64 + kClasses) * 8 >= (1ll << 31) - (1ll << 20)) C = 1;
   g->C = C;
@@ -573,7 +588,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_HIP(hipMemsetAsync(nlight.p, 0, sizeof(unsigned long long), s));
   unsigned long long n_light = 0;
   if (V > 0) {
-    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, bd, maxd, C > 1,
+    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, bd, maxd, C > 1, heavy_min_setting(),
                        c_deg.as<int32_t>(), c_rowptr.as<int64_t>(), vk.as<uint64_t>(),
                        nlight.as<unsigned long long>());
     PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd + 1, s));
@@ -595,7 +610,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     const int64_t Hp = H_total > part ? (H_total - part + P - 1) / P : 0;
     geo.hcum[0] = 0;
     for (int x = 0; x < C; ++x) geo.hcum[x + 1] = geo.hcum[x] + (Hp > x ? (Hp - x + C - 1) / C : 0);
-    for (int x = C; x < kClasses; ++x) geo.hcum[x + 1] = geo.hcum[x];
+    for (int x = C; x < kMaxClasses; ++x) geo.hcum[x + 1] = geo.hcum[x];
   }
   g->geo = geo;
   g->n_heavy = geo.hcum[C];
@@ -687,7 +702,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
       plan_wave_units(rp, x, kWavePT, &wp, &pieces, &seg_cls, &seg_row, &seg_p0);
     }
   }
-  wp.ucum.resize(kClasses + 1, (int64_t)wp.units.size());
+  wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
   lr_p0.push_back((int32_t)pieces);
   keys.reset();
   tmp.reset();
@@ -701,6 +716,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   {
     const int slots = hot_slots_setting();
     HotGeom hg{};
+    hg.C = C;
     hg.P = P;
     hg.Kp = C > 1 ? slots / P : 0;
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
@@ -709,16 +725,16 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->hot = hg;
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
-    g->hot_grid = std::max(kClasses, n_cu / kClasses * kClasses);
+    g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
     PR_TRY(prepare_hot_kernel());
     const size_t nu = wp.units.size();
     g->n_hunits = (int64_t)nu;
     PR_TRY(g->hunits.alloc(sizeof(Unit) * (nu + 1)));
     PR_HIP(hipMemsetAsync(g->hunits.p, 0, sizeof(Unit) * (nu + 1), s));  // unit nu: the empty unit
-    PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kClasses + 1)));
+    PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->colh.alloc(sizeof(uint32_t) * (wp.len > 0 ? wp.len : 8)));
     PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
-    PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kClasses + 1), hipMemcpyHostToDevice, s));
+    PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     if (nu > 0) {
       DevBuf dsrc_off, dcls, dlo;
       PR_TRY(dsrc_off.alloc(sizeof(int64_t) * nu));

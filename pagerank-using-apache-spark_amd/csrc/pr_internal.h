@@ -91,7 +91,9 @@ __host__ __device__ inline int unit_n(const Unit &u) { return u.n & 0xFFFF; }
 __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
-constexpr int kClasses = 8;                          // one per XCD of the MI355X
+constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
+constexpr int kClasses = 8;                          // classes of the fused-kernel era: one per XCD
+constexpr int kMaxClasses = 16;                      // two per XCD: the default
 constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once c outgrows the 8 x 4 MiB L2s
 
 // per-row info word: out-degree | flags
@@ -102,7 +104,7 @@ constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
 constexpr uint32_t kRowHeavy = 1u << 31;   // class-split row (its sum comes from the epilogue)
 // Only rows with at least this many in-links are split by class: a split row costs C partial
 // slots (write + read) and C row lengths, worth it only when enough gathers gain L2 locality.
-constexpr int kHeavyMinIndeg = 8;
+constexpr int kHeavyMinIndeg = 16;
 
 // ---- heavy rows: wave units with an LDS-resident hot set (pr_spmv.h k_spmv_hot) -------------
 // A wave unit is one wavefront's work: kWavePT in-link entries per lane, kWaveUnit entries in
@@ -134,7 +136,7 @@ constexpr int kHotSlotsDefault = kHotSlotsMax;  // 16382 hot contributions (128 
 struct ClassGeom {
   int C;
   int64_t Q_pad, S_pad;
-  int64_t hcum[kClasses + 1];  // heavy rows in regions < x (heavy rows are a prefix of a region)
+  int64_t hcum[kMaxClasses + 1];  // heavy rows in regions < x (heavy rows are a prefix of a region)
   __host__ __device__ int64_t heavy_to_row(int64_t h) const {
     int y = 0;
     while (y + 1 < C && hcum[y + 1] <= h) ++y;
@@ -145,7 +147,7 @@ struct ClassGeom {
 // Where a class's hot contributions live in the gather space: for every part p, positions
 // [p*S_pad + x*Q_pad, + q_load) go to LDS slots 1 + [p*Kp, p*Kp + q_load); slot 0 holds 0.0.
 struct HotGeom {
-  int P, Kp, q_load;
+  int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;
   __host__ __device__ int slots() const { return P * Kp + 1; }
   __host__ __device__ int stage_off() const { return (slots() + 1) & ~1; }  // 16-byte aligned

@@ -223,7 +223,8 @@ int iter_compute(pr_graph *g) {
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_row.as<int32_t>(), g->seg_cls.as<int32_t>(), g->seg_p0.as<int32_t>(),
                          g->piece_part.as<double>(), g->partial.as<double>(), H);
-    hipLaunchKernelGGL(k_epilogue<kClasses>, dim3(g->ep_blocks), dim3(kThreads), 0, s, H, g->geo,
+    hipLaunchKernelGGL(g->C == kMaxClasses ? k_epilogue<kMaxClasses> : k_epilogue<kClasses>, dim3(g->ep_blocks),
+                       dim3(kThreads), 0, s, H, g->geo,
                        g->partial.as<double>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
                        g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->nparts,
                        (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);

@@ -402,8 +402,9 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           double *__restrict__ partial,
                                                           double *__restrict__ piece_part, int64_t H) {
   extern __shared__ double hot[];
-  const int x = (int)(blockIdx.x % kClasses);
-  const int team = (int)(blockIdx.x / kClasses), nteams = (int)(gridDim.x / kClasses);
+  // class x runs on XCD x % 8 (round-robin dispatch: workgroup b on XCD b % 8)
+  const int x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
+  const int team = (int)(blockIdx.x / hg.C), nteams = (int)(gridDim.x / hg.C);
   // stage the class's hot contributions (the previous iteration's, final before this launch)
   const int nh = hg.P * hg.Kp;
   for (int i = threadIdx.x; i < nh; i += kHotThreads) {
@@ -421,13 +422,13 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   const int64_t stride = (int64_t)nteams * (kHotThreads / kWave);
   int64_t k = beg + (int64_t)team * (kHotThreads / kWave) + wv;
   if (k >= end) return;
-  // unit descriptors through the scalar cache; index n_units (= ucum[kClasses]) is an empty unit
+  // unit descriptors through the scalar cache; index n_units (= ucum[kMaxClasses]) is an empty unit
   const __attribute__((address_space(4))) pr_v4i *cu = (const __attribute__((address_space(4))) pr_v4i *)units;
   auto unit_at = [&](int64_t i) -> Unit {
     const pr_v4i q = cu[i];
     return Unit{(uint32_t)q.x, q.y, q.z, q.w};
   };
-  const int64_t none_k = ucum[kClasses];
+  const int64_t none_k = ucum[kMaxClasses];
   // ring of three units: codes of i+2 and values of i+1 in flight while unit i is reduced
   Unit u[3];
   WaveCodes wc[3];

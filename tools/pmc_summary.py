@@ -13,7 +13,7 @@ import os
 import sys
 
 # the SpMV pass of one iteration = these kernels (pr_iter.hip iter_compute)
-PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue", "k_finalize")
+PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue")
 KERNEL = "k_spmv_hot"
 
 
