@@ -113,19 +113,12 @@ __global__ void k_vflags(int32_t V, const uint8_t *__restrict__ is_key,
   atomicMax(&cnt[4], mo);
 }
 
-// Internal order key: heavy before light (split layout only), then out-degree descending,
-// original ID ascending.  *n_light counts the light vertices.
-__global__ void k_order_keys(int32_t V, int b, int bd, uint64_t maxd, bool split, int heavy_min,
-                             const int32_t *__restrict__ deg, const int64_t *__restrict__ rowptr,
-                             uint64_t *__restrict__ vk, unsigned long long *__restrict__ n_light) {
-  unsigned long long nl = 0;
+// Internal order key: out-degree descending, original ID ascending (hot contributions first).
+__global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
+                             uint64_t *__restrict__ vk) {
   for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V;
-       v += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t light = (split && rowptr[v + 1] - rowptr[v] < heavy_min) ? 1ull : 0ull;
-    nl += light;
-    vk[v] = (light << (b + bd)) | ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
-  }
-  atomicAdd(n_light, nl);
+       v += (int64_t)gridDim.x * blockDim.x)
+    vk[v] = ((maxd - (uint64_t)deg[v]) << b) | (uint64_t)v;
 }
 
 // rank_of[v] = sorted index; gpos[v] = gather position of v's contribution.  Sorted index i
@@ -152,8 +145,7 @@ struct PartPred {
   }
 };
 // local key = (segment << (brow + bg)) | (row << bg) | gather position of src, where the
-// segment is the class of the source for a heavy destination row (row = heavy index h) and C
-// for a light one (row = local row L).
+// segment is the column class of the source (0 in the fused layout) and row the local row L.
 struct PartXform {
   const uint64_t *k;
   const int32_t *gpos;
@@ -164,13 +156,8 @@ struct PartXform {
     const uint64_t key = k[i];
     const int32_t d = (int32_t)(key >> b), s = (int32_t)(key & mask);
     const int64_t gs = gpos[s];
-    const int64_t L = gpos[d] % geo.S_pad;
-    const int64_t xd = L / geo.Q_pad, qd = L % geo.Q_pad;
-    uint64_t seg = (uint64_t)geo.C, row = (uint64_t)L;
-    if (geo.C > 1 && qd < geo.hcum[xd + 1] - geo.hcum[xd]) {
-      seg = (uint64_t)((gs % geo.S_pad) / geo.Q_pad);
-      row = (uint64_t)(geo.hcum[xd] + qd);
-    }
+    const uint64_t row = (uint64_t)(gpos[d] % geo.S_pad);
+    const uint64_t seg = geo.C > 1 ? (uint64_t)((gs % geo.S_pad) / geo.Q_pad) : 0ull;
     return (seg << (brow + bg)) | (row << bg) | (uint64_t)gs;
   }
 };
@@ -224,7 +211,6 @@ __global__ void k_local_rows(int64_t R, int64_t n_local, int P, int part, ClassG
     uint32_t info = (uint32_t)deg[v];
     if (deg[v] == 0 && (vflags[v] & PR_VF_SINK) && !dangling_none) info |= kRowSink;
     if (vflags[v] & PR_VF_INDEG0) info |= kRowIndeg0;
-    if (C > 1 && q < geo.hcum[x + 1] - geo.hcum[x]) info |= kRowHeavy;
     rowinfo[L] = info;
   }
 }
@@ -307,52 +293,64 @@ int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, h
   return PR_OK;
 }
 
-// ---- heavy rows: wave units + entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) ----------------
+// ---- split layout: wave units + entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) -----------
 struct WavePlan {
-  std::vector<Unit> units;       // p8 = entry offset / 8, r0 = first heavy row, meta, n = padded entries
-  std::vector<int64_t> src_off;  // first in-link of the unit in its class's CSR
-  std::vector<int32_t> cls;
+  std::vector<Unit> units;       // p8 = entry offset / 8, r0 = first slot, meta, n = padded entries
+  std::vector<int64_t> src_off;  // first in-link of the unit in the part's column array
+  std::vector<int32_t> n_real;   // in-links of the unit (without padding)
   std::vector<int64_t> ucum;     // units of class < x
   int64_t len = 0;               // entries (padded)
 };
 
-// Greedy, linear, deterministic: consecutive whole segments (empty ones count one dummy entry)
-// while they fit kWaveUnit entries; a segment longer than kWaveUnit becomes PIECE units.
-static void plan_wave_units(const std::vector<int64_t> &rp, int x, int pt, WavePlan *wp, int64_t *pieces,
-                            std::vector<int32_t> *seg_cls, std::vector<int32_t> *seg_row,
-                            std::vector<int32_t> *seg_p0) {
-  const int64_t H = (int64_t)rp.size() - 1, cap = (int64_t)kWave * pt;
+// Class x of one part: segments = rows with at least one class-x in-link, in row order; segment
+// k has slot k (its partial sum lands in part_x[k]).  Greedy, linear, deterministic: consecutive
+// segments while they fit kWaveUnit entries; a longer segment becomes PIECE units.  Also records
+// base[blk][x] (stride C) = slot of the first segment at or after row 64*blk (the epilogue's
+// slot lookup).
+static void plan_class_units(const std::vector<int64_t> &rp, int64_t lo, int x, int C, WavePlan *wp, int64_t *pieces,
+                             std::vector<int32_t> *seg_cls, std::vector<int64_t> *seg_slot,
+                             std::vector<int32_t> *seg_p0, int32_t *base, int64_t *n_slots) {
+  const int64_t R = (int64_t)rp.size() - 1, cap = kWaveUnit;
   auto push = [&](int64_t src, int64_t r0, int64_t meta, int64_t n) {
-    const int64_t np = (n + pt - 1) / pt * pt;
+    const int64_t np = (n + kWavePT - 1) / kWavePT * kWavePT;
     wp->units.push_back(Unit{(uint32_t)(wp->len / 8), (int32_t)r0, (int32_t)meta, (int32_t)np});
-    wp->src_off.push_back(src);
-    wp->cls.push_back(x);
+    wp->src_off.push_back(lo + src);
+    wp->n_real.push_back((int32_t)n);
     wp->len += np;
   };
-  int64_t h = 0;
-  while (h < H) {
-    const int64_t len = rp[h + 1] - rp[h];
+  int64_t slot = 0, u_r0 = 0, u_src = 0, u_n = 0, u_seg = 0;
+  auto flush = [&]() {
+    if (u_seg > 0) push(u_src, u_r0, u_seg, u_n);
+    u_seg = 0;
+    u_n = 0;
+  };
+  for (int64_t L = 0; L < R; ++L) {
+    if ((L & 63) == 0) base[(L >> 6) * C] = (int32_t)slot;
+    const int64_t len = rp[L + 1] - rp[L];
+    if (len == 0) continue;
     if (len > cap) {
+      flush();
       const int64_t np = (len + cap - 1) / cap;
       seg_cls->push_back(x);
-      seg_row->push_back((int32_t)h);
+      seg_slot->push_back(slot);
       seg_p0->push_back((int32_t)*pieces);
       for (int64_t q = 0; q < np; ++q)
-        push(rp[h] + q * cap, h, -(*pieces + q) - 1, std::min<int64_t>(cap, len - q * cap));
+        push(rp[L] + q * cap, slot, -(*pieces + q) - 1, std::min<int64_t>(cap, len - q * cap));
       *pieces += np;
-      ++h;
+      ++slot;
       continue;
     }
-    const int64_t start = h;
-    int64_t n = 0;
-    while (h < H) {
-      const int64_t l = rp[h + 1] - rp[h];
-      if (l > cap || n + std::max<int64_t>(l, 1) > cap) break;
-      n += std::max<int64_t>(l, 1);
-      ++h;
+    if (u_seg > 0 && u_n + len > cap) flush();
+    if (u_seg == 0) {
+      u_r0 = slot;
+      u_src = rp[L];
     }
-    push(rp[start], start, h - start, n);
+    u_n += len;
+    ++u_seg;
+    ++slot;
   }
+  flush();
+  *n_slots = slot;
 }
 
 // Entry code (pr_internal.h); a segment end is marked in bit 0 until k_unit_meta moves it into
@@ -363,55 +361,49 @@ __device__ __forceinline__ uint32_t hot_code(int32_t pos, int x, const HotGeom &
   return end ? (c | 1u) : c;
 }
 
-// One workgroup per wave unit: writes its entry codes (segment ends, dummies, padding).
-__global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, int cap, const Unit *__restrict__ units,
+// Marks the last in-link of every non-empty row of a class CSR (bit 31 of the column entry;
+// gather positions are < 2^28 in the split layout).
+__global__ void k_mark_ends(int64_t R, const int64_t *__restrict__ rp, int32_t *__restrict__ col) {
+  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = rp[L + 1];
+    if (e > rp[L]) col[e - 1] |= (int32_t)0x80000000u;
+  }
+}
+
+// Row class masks: bit x when the row has a class-x in-link.
+__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, uint16_t *__restrict__ rmask) {
+  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+    for (int x = 0; x < C; ++x) {
+      const int64_t *rp = rp_all + (int64_t)x * (R + 1);
+      if (rp[L + 1] > rp[L]) m |= 1u << x;
+    }
+    rmask[L] = (uint16_t)m;
+  }
+}
+
+// One workgroup per wave unit: its entry codes (end marks in bit 0, padding 0).
+__global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *__restrict__ units,
                                                   const int64_t *__restrict__ src_off,
-                                                  const int32_t *__restrict__ ucls,
-                                                  const int64_t *__restrict__ rp_all, int64_t H,
-                                                  const int64_t *__restrict__ cls_lo,
+                                                  const int32_t *__restrict__ n_real,
                                                   const int32_t *__restrict__ col, HotGeom hg,
+                                                  const int64_t *__restrict__ ucum,
                                                   uint32_t *__restrict__ colh) {
-  __shared__ uint32_t scratch[256 / kWave];
-  const uint32_t zero = kEntZero;
   for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
     const Unit u = units[b];
-    const int x = ucls[b];
-    const int64_t *rp = rp_all + (int64_t)x * (H + 1);
-    const int32_t *cx = col + cls_lo[x];
+    int x = 0;
+    while (x + 1 < hg.C && ucum[x + 1] <= b) ++x;
     uint32_t *dst = colh + (int64_t)u.p8 * 8;
-    const int npad = u.n;
-    if (u.meta < 0) {
-      const int64_t s0 = src_off[b];
-      const int64_t n = min((int64_t)cap, rp[u.r0 + 1] - s0);
-      for (int i = threadIdx.x; i < npad; i += 256) dst[i] = i < n ? hot_code(cx[s0 + i], x, hg, false) : zero;
-      continue;
-    }
-    const int nr = u.meta;  // <= cap <= 1024 rows: four per thread
-    const int r_a = 4 * threadIdx.x;
-    int64_t ln[4];
-    uint32_t ef[4], sum = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int r = r_a + k;
-      ln[k] = r < nr ? rp[u.r0 + r + 1] - rp[u.r0 + r] : 0;
-      ef[k] = r < nr ? (uint32_t)max(ln[k], (int64_t)1) : 0u;
-      sum += ef[k];
-    }
-    uint32_t tot;
-    uint32_t off = block_exclusive_scan<256>(sum, scratch, &tot);
-    for (int k = 0; k < 4; ++k) {
-      const int r = r_a + k;
-      if (r >= nr) break;
-      const int64_t len = ln[k];
-      if (len == 0) {
-        dst[off] = zero | 1u;  // dummy: the row has no class-x in-link
-      } else {
-        const int64_t s0 = rp[u.r0 + r];
-        for (int64_t i = 0; i < len; ++i) dst[off + i] = hot_code(cx[s0 + i], x, hg, i == len - 1);
+    const int64_t s0 = src_off[b];
+    const int n = n_real[b];
+    for (int i = threadIdx.x; i < u.n; i += 256) {
+      uint32_t c = 0;
+      if (i < n) {
+        const int32_t v = col[s0 + i];
+        c = hot_code(v & 0x7FFFFFFF, x, hg, u.meta >= 0 && v < 0);
       }
-      off += ef[k];
+      dst[i] = c;
     }
-    for (int i = (int)tot + threadIdx.x; i < npad; i += 256) dst[i] = zero;
   }
 }
 
@@ -453,17 +445,11 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 }
 
 // Tuning knobs read at build time: column classes of the split layout (8 = one
-// per XCD, 16 = two per XCD) and the in-degree from which a row is class-split.
+// per XCD, 16 = two per XCD) and the size of the LDS hot set.
 static int class_setting() {
   int c = kMaxClasses;
   if (const char *e = getenv("PR_CLASSES")) c = atoi(e);
   return c == 16 ? 16 : 8;
-}
-
-static int heavy_min_setting() {
-  int h = kHeavyMinIndeg;
-  if (const char *e = getenv("PR_HEAVY_MIN")) h = atoi(e);
-  return std::max(1, h);
 }
 
 static int hot_slots_setting() {
@@ -570,56 +556,40 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
   if (g->flags & PR_LAYOUT_SPLIT) C = c_split;
   // heavy-row entry codes are byte offsets below 2^31 (pr_internal.h)
-  if ((int64_t)P * (g->n_local_max + 64 + kClasses) * 8 >= (1ll << 31) - (1ll << 20)) C = 1;
+  if ((int64_t)P * (g->n_local_max + 64 + kMaxClasses) * 8 >= (1ll << 31) - (1ll << 20)) C = 1;
   g->C = C;
   g->Q_pad = (g->n_local_max + C - 1) / C;
-  if (g->Q_pad < 1) g->Q_pad = 1;
+  g->Q_pad = (g->Q_pad + 63) / 64 * 64;  // rows come in whole 64-row blocks (k_epilogue)
   g->n_rows = (int64_t)C * g->Q_pad;
   g->S_pad = ((g->n_rows + 2 + 63) / 64) * 64;
   if ((int64_t)P * g->S_pad >= (int64_t(1) << 31)) return fail(PR_ERR_INVALID, "gather space exceeds 2^31 entries");
   const int bd = bits_for(max_outdeg);
   const uint64_t maxd = (uint64_t(1) << bd) - 1;
-  DevBuf vk, vtmp, rank_of, gpos, nlight;
+  DevBuf vk, vtmp, rank_of, gpos;
   PR_TRY(vk.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
   PR_TRY(vtmp.alloc(sizeof(uint64_t) * ((size_t)V + 1)));
   PR_TRY(rank_of.alloc(sizeof(int32_t) * ((size_t)V + 1)));
   PR_TRY(gpos.alloc(sizeof(int32_t) * ((size_t)V + 1)));
-  PR_TRY(nlight.alloc(sizeof(unsigned long long)));
-  PR_HIP(hipMemsetAsync(nlight.p, 0, sizeof(unsigned long long), s));
-  unsigned long long n_light = 0;
   if (V > 0) {
-    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, bd, maxd, C > 1, heavy_min_setting(),
-                       c_deg.as<int32_t>(), c_rowptr.as<int64_t>(), vk.as<uint64_t>(),
-                       nlight.as<unsigned long long>());
-    PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd + 1, s));
+    hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, maxd, c_deg.as<int32_t>(),
+                       vk.as<uint64_t>());
+    PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd, s));
     hipLaunchKernelGGL(k_rank_gpos, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, maskb, P, C,
                        g->Q_pad, g->S_pad, vk.as<uint64_t>(), rank_of.as<int32_t>(), gpos.as<int32_t>());
     PR_HIP(hipGetLastError());
-    PR_HIP(hipMemcpyAsync(&n_light, nlight.p, sizeof(n_light), hipMemcpyDeviceToHost, s));
-    PR_HIP(hipStreamSynchronize(s));
   }
   vtmp.reset();
-  // heavy vertices sort first: part p owns sorted ranks i = p, p+P, ...; its heavy local ranks are
-  // j < Hp, and class x gets the heavy prefix q < H_x of its region
   ClassGeom geo{};
   geo.C = C;
   geo.Q_pad = g->Q_pad;
   geo.S_pad = g->S_pad;
-  {
-    const int64_t H_total = C > 1 ? (int64_t)V - (int64_t)n_light : 0;  // fused: no heavy rows
-    const int64_t Hp = H_total > part ? (H_total - part + P - 1) / P : 0;
-    geo.hcum[0] = 0;
-    for (int x = 0; x < C; ++x) geo.hcum[x + 1] = geo.hcum[x] + (Hp > x ? (Hp - x + C - 1) / C : 0);
-    for (int x = C; x < kMaxClasses; ++x) geo.hcum[x + 1] = geo.hcum[x];
-  }
   g->geo = geo;
-  g->n_heavy = geo.hcum[C];
 
-  // ---- the part's in-link CSRs: one per class over heavy rows, one over light rows ----
-  const int64_t R = g->n_rows, H = g->n_heavy;
+  // ---- the part's in-link CSRs: one per column class (one in the fused layout) ----
+  const int64_t R = g->n_rows;
   const int bg = bits_for((uint64_t)P * g->S_pad);
   const int brow = bits_for((uint64_t)R);
-  const int bseg = bits_for((uint64_t)C + 1);
+  const int bseg = bits_for((uint64_t)C);
   const uint64_t maskg = (uint64_t(1) << bg) - 1;
   int64_t lm = 0;
   PR_TRY(compact_index(m, PartPred{ukeys, rank_of.as<int32_t>(), b, P, part},
@@ -632,11 +602,11 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
                        keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
   DevBuf cls_start;
-  PR_TRY(cls_start.alloc(sizeof(int64_t) * (C + 2)));
+  PR_TRY(cls_start.alloc(sizeof(int64_t) * (C + 1)));
   hipLaunchKernelGGL(k_class_bounds, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s,
-                     keys.as<uint64_t>(), lm, bg + brow, C + 1, cls_start.as<int64_t>());
-  std::vector<int64_t> hcls(C + 2);
-  PR_HIP(hipMemcpyAsync(hcls.data(), cls_start.p, sizeof(int64_t) * (C + 2), hipMemcpyDeviceToHost, s));
+                     keys.as<uint64_t>(), lm, bg + brow, C, cls_start.as<int64_t>());
+  std::vector<int64_t> hcls(C + 1);
+  PR_HIP(hipMemcpyAsync(hcls.data(), cls_start.p, sizeof(int64_t) * (C + 1), hipMemcpyDeviceToHost, s));
   PR_HIP(hipStreamSynchronize(s));
   PR_TRY(g->rowinfo.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
   DevBuf orig;
@@ -650,75 +620,80 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   rank_of.reset();
   gpos.reset();
 
-  // ---- work plans (host greedy) + one padded gather-position array for all units ----
-  UnitPlan all;  // src offsets / padded offsets of every unit, for build_padded_cols
+  // ---- work plans (host greedy) ----
   const uint64_t rmask = (uint64_t(1) << brow) - 1;
-  DevBuf rp_dev;
-  PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
   std::vector<int64_t> rp;
-  std::vector<int32_t> seg_cls, seg_row, seg_p0;
-  std::vector<Unit> light_units;
+  std::vector<int32_t> seg_cls, seg_p0;
+  std::vector<int64_t> seg_slot;
   std::vector<int32_t> lr_row, lr_p0;
-  int64_t pieces = 0, padded = 0;
-  // heavy rows: per-class row pointers stay on the device for the code fill
+  std::vector<Unit> light_units;
+  int64_t pieces = 0;
   WavePlan wp;
-  DevBuf rp_all;
-  if (C > 1 && H > 0) PR_TRY(rp_all.alloc(sizeof(int64_t) * (size_t)C * (H + 1)));
-  for (int x = 0; x <= C; ++x) {
-    const bool light = (x == C);
-    const int64_t lo = hcls[x], hi = hcls[x + 1], rows = light ? R : H;
-    if (!light) wp.ucum.push_back((int64_t)wp.units.size());
-    else seg_p0.push_back((int32_t)pieces);  // end of the heavy pieces
-    if (!light && (C == 1 || H == 0)) continue;
-    int64_t *rpd = light ? rp_dev.as<int64_t>() : rp_all.as<int64_t>() + (size_t)x * (H + 1);
-    hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(hi - lo + 1, T, 65536)), dim3(T), 0, s,
-                       keys.as<uint64_t>(), lo, hi, bg, rmask, rows, rpd);
+  g->nblk = (R + 63) / 64;
+  std::vector<int32_t> hbase;
+  std::vector<int64_t> poff(kMaxClasses + 1, 0);
+  if (C == 1) {
+    // fused layout: one CSR over all rows, 256-thread units with the fused epilogue
+    DevBuf rp_dev;
+    PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
+    hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s, keys.as<uint64_t>(),
+                       (int64_t)0, lm, bg, rmask, R, rp_dev.as<int64_t>());
     PR_HIP(hipGetLastError());
-    rp.assign((size_t)rows + 1, 0);
-    PR_HIP(hipMemcpyAsync(rp.data(), rpd, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
+    rp.assign((size_t)R + 1, 0);
+    PR_HIP(hipMemcpyAsync(rp.data(), rp_dev.p, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
     PR_HIP(hipStreamSynchronize(s));
-    if (light) {
-      UnitPlan px;
-      PR_TRY(g->rowptr.alloc(sizeof(int64_t) * ((size_t)R + 1)));
-      PR_HIP(hipMemcpyAsync(g->rowptr.p, rp_dev.p, sizeof(int64_t) * ((size_t)R + 1), hipMemcpyDeviceToDevice, s));
-      // light rows: region y's rows after its heavy prefix (holes are planned too, at no cost)
-      for (int y = 0; y < C; ++y)
-        plan_units(rp, kUnitNnz, kUnitRows, &px, (int64_t)y * g->Q_pad + (geo.hcum[y + 1] - geo.hcum[y]),
-                   (int64_t)(y + 1) * g->Q_pad, true);
-      for (size_t q = 0; q + 1 < px.lr_p0.size(); ++q) {
-        lr_row.push_back(px.lr_row[q]);
-        lr_p0.push_back((int32_t)(px.lr_p0[q] + pieces));
-      }
-      for (size_t k = 0; k < px.units.size(); ++k) {
-        Unit u = px.units[k];
-        if (u.meta < 0) u.meta -= (int32_t)pieces;  // global piece index
-        light_units.push_back(u);
-        all.units.push_back(u);
-        all.src_off.push_back(px.src_off[k] + lo);
-      }
-      pieces += px.n_pieces;
-      padded += px.padded_len;
-    } else {
-      plan_wave_units(rp, x, kWavePT, &wp, &pieces, &seg_cls, &seg_row, &seg_p0);
+    keys.reset();
+    tmp.reset();
+    UnitPlan px;
+    plan_units(rp, kUnitNnz, kUnitRows, &px);
+    g->rowptr = std::move(rp_dev);
+    lr_row = px.lr_row;
+    lr_p0 = px.lr_p0;
+    light_units = px.units;
+    pieces = px.n_pieces;
+    if (px.padded_len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+    PR_TRY(g->colp.alloc(sizeof(int32_t) * (px.padded_len > 0 ? px.padded_len : 8)));
+    PR_TRY(build_padded_cols(px, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
+    seg_p0.push_back(0);
+  } else {
+    // split layout: per class, the segments of the rows with class-x in-links -> wave units
+    DevBuf rp_all;
+    PR_TRY(rp_all.alloc(sizeof(int64_t) * (size_t)C * (R + 1)));
+    hbase.assign((size_t)C * g->nblk, 0);
+    for (int x = 0; x < C; ++x) {
+      int64_t *rpd = rp_all.as<int64_t>() + (size_t)x * (R + 1);
+      hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(hcls[x + 1] - hcls[x] + 1, T, 65536)), dim3(T), 0, s,
+                         keys.as<uint64_t>(), hcls[x], hcls[x + 1], bg, rmask, R, rpd);
+      hipLaunchKernelGGL(k_mark_ends, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, rpd,
+                         g->col.as<int32_t>() + hcls[x]);
+      PR_HIP(hipGetLastError());
+      rp.assign((size_t)R + 1, 0);
+      PR_HIP(hipMemcpyAsync(rp.data(), rpd, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
+      PR_HIP(hipStreamSynchronize(s));
+      wp.ucum.push_back((int64_t)wp.units.size());
+      int64_t n_slots = 0;
+      plan_class_units(rp, hcls[x], x, C, &wp, &pieces, &seg_cls, &seg_slot, &seg_p0, hbase.data() + x, &n_slots);
+      poff[x + 1] = poff[x] + n_slots;
+      if (n_slots >= (int64_t(1) << 29)) return fail(PR_ERR_INVALID, "a column class exceeds 2^29 segments");
     }
-  }
-  wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
-  lr_p0.push_back((int32_t)pieces);
-  keys.reset();
-  tmp.reset();
-  all.padded_len = padded;
-  all.n_pieces = pieces;
-  if (all.padded_len / 8 >= (int64_t(1) << 32) || wp.len / 8 >= (int64_t(1) << 32))
-    return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
-  PR_TRY(g->colp.alloc(sizeof(int32_t) * (all.padded_len > 0 ? all.padded_len : 8)));
-  PR_TRY(build_padded_cols(all, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
-  // heavy wave units: LDS hot set per class, then the entry codes
-  {
+    keys.reset();
+    tmp.reset();
+    for (int x = C; x < kMaxClasses; ++x) poff[x + 1] = poff[x];
+    wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
+    seg_p0.push_back((int32_t)pieces);
+    for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
+    PR_TRY(g->rmask.alloc(sizeof(uint16_t) * ((size_t)R + 1)));
+    hipLaunchKernelGGL(k_row_masks, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
+                       g->rmask.as<uint16_t>());
+    PR_HIP(hipGetLastError());
+    rp_all.reset();
+    if (wp.len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+    // LDS hot set per class, then the entry codes
     const int slots = hot_slots_setting();
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
-    hg.Kp = C > 1 ? slots / P : 0;
+    hg.Kp = slots / P;
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
@@ -732,39 +707,43 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->hunits.alloc(sizeof(Unit) * (nu + 1)));
     PR_HIP(hipMemsetAsync(g->hunits.p, 0, sizeof(Unit) * (nu + 1), s));  // unit nu: the empty unit
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
+    PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->colh.alloc(sizeof(uint32_t) * (wp.len > 0 ? wp.len : 8)));
     PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
+    PR_TRY(g->cbase.alloc(sizeof(int32_t) * (hbase.size() + 1)));
+    PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] > 0 ? poff[C] : 1)));
+    g->n_slots = poff[C];
+    for (int x = 0; x <= kMaxClasses; ++x) g->part_off.o[x] = poff[x];
     PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
+    PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
+    if (!hbase.empty())
+      PR_HIP(hipMemcpyAsync(g->cbase.p, hbase.data(), sizeof(int32_t) * hbase.size(), hipMemcpyHostToDevice, s));
     if (nu > 0) {
-      DevBuf dsrc_off, dcls, dlo;
+      DevBuf dsrc_off, dn;
       PR_TRY(dsrc_off.alloc(sizeof(int64_t) * nu));
-      PR_TRY(dcls.alloc(sizeof(int32_t) * nu));
-      PR_TRY(dlo.alloc(sizeof(int64_t) * (C + 2)));
+      PR_TRY(dn.alloc(sizeof(int32_t) * nu));
       PR_HIP(hipMemcpyAsync(g->hunits.p, wp.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
       PR_HIP(hipMemcpyAsync(dsrc_off.p, wp.src_off.data(), sizeof(int64_t) * nu, hipMemcpyHostToDevice, s));
-      PR_HIP(hipMemcpyAsync(dcls.p, wp.cls.data(), sizeof(int32_t) * nu, hipMemcpyHostToDevice, s));
-      PR_HIP(hipMemcpyAsync(dlo.p, hcls.data(), sizeof(int64_t) * (C + 2), hipMemcpyHostToDevice, s));
+      PR_HIP(hipMemcpyAsync(dn.p, wp.n_real.data(), sizeof(int32_t) * nu, hipMemcpyHostToDevice, s));
       hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(256), 0, s, (int64_t)nu,
-                         kWaveUnit,
-                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dcls.as<int32_t>(), rp_all.as<int64_t>(), H,
-                         dlo.as<int64_t>(), g->col.as<int32_t>(), hg, g->colh.as<uint32_t>());
+                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dn.as<int32_t>(), g->col.as<int32_t>(), hg,
+                         g->hucum.as<int64_t>(), g->colh.as<uint32_t>());
       hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(kWave), 0, s, (int64_t)nu,
                          g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
       PR_HIP(hipGetLastError());
       PR_HIP(hipStreamSynchronize(s));
     }
   }
-  rp_all.reset();
   g->col.reset();
+  if (lr_p0.empty()) lr_p0.push_back((int32_t)pieces);
   g->n_units = (int64_t)light_units.size();
   g->n_long = (int64_t)lr_row.size();
-  g->n_segs = (int64_t)seg_row.size();
+  g->n_segs = (int64_t)seg_slot.size();
   g->n_pieces = pieces;
   PR_TRY(g->units.alloc(sizeof(Unit) * (light_units.size() + 1)));
   PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (lr_row.size() + 1)));
   PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (lr_p0.size() + 1)));
-  PR_TRY(g->seg_row.alloc(sizeof(int32_t) * (seg_row.size() + 1)));
-  PR_TRY(g->seg_cls.alloc(sizeof(int32_t) * (seg_cls.size() + 1)));
+  PR_TRY(g->seg_slot.alloc(sizeof(int64_t) * (seg_slot.size() + 1)));
   PR_TRY(g->seg_p0.alloc(sizeof(int32_t) * (seg_p0.size() + 1)));
   PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
   if (!light_units.empty())
@@ -772,12 +751,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   if (!lr_row.empty())
     PR_HIP(hipMemcpyAsync(g->lr_row.p, lr_row.data(), sizeof(int32_t) * lr_row.size(), hipMemcpyHostToDevice, s));
   PR_HIP(hipMemcpyAsync(g->lr_p0.p, lr_p0.data(), sizeof(int32_t) * lr_p0.size(), hipMemcpyHostToDevice, s));
-  if (!seg_row.empty()) {
-    PR_HIP(hipMemcpyAsync(g->seg_row.p, seg_row.data(), sizeof(int32_t) * seg_row.size(), hipMemcpyHostToDevice, s));
-    PR_HIP(hipMemcpyAsync(g->seg_cls.p, seg_cls.data(), sizeof(int32_t) * seg_cls.size(), hipMemcpyHostToDevice, s));
-  }
+  if (!seg_slot.empty())
+    PR_HIP(hipMemcpyAsync(g->seg_slot.p, seg_slot.data(), sizeof(int64_t) * seg_slot.size(), hipMemcpyHostToDevice, s));
   PR_HIP(hipMemcpyAsync(g->seg_p0.p, seg_p0.data(), sizeof(int32_t) * seg_p0.size(), hipMemcpyHostToDevice, s));
-  if (C > 1) PR_TRY(g->partial.alloc(sizeof(double) * (size_t)C * (H > 0 ? H : 1)));
   g->orig_of_local.resize((size_t)R);
   if (R > 0)
     PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * R, hipMemcpyDeviceToHost, s));
@@ -794,8 +770,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
-  g->ep_blocks = (int)grid_for(g->n_heavy > 0 ? g->n_heavy : 1, 256, 2048);
-  // finalize input: light-unit partials followed by the split epilogue's block partials
+  g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
+  // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 

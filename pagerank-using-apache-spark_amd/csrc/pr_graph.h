@@ -59,14 +59,18 @@ struct pr_graph {
 
   // part layout
   pr::DevBuf rowptr, col, colp, rowinfo, r;
-  // heavy rows (C > 1): wave units per class (hunits[hucum[x], hucum[x+1])), their entry codes,
-  // per-class partial sums partial[x][h], long segments (seg_*: pieces reduced in order)
-  pr::DevBuf colh, hmeta, hunits, hucum, partial, seg_row, seg_cls, seg_p0;
+  // split layout (C > 1): wave units per class (hunits[hucum[x], hucum[x+1])), their entry codes
+  // and lane metadata; per class x the partial sums of its segments at partial[poff[x] + slot];
+  // per row the mask of classes with in-links (rmask) and per class the slot of the first
+  // segment of every 64-row block (cbase[blk][x]); long segments: pieces reduced in order into
+  // partial[seg_slot[q]]
+  pr::DevBuf colh, hmeta, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0;
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};
-  int hot_grid = 0;  // workgroups of k_spmv_hot (a multiple of 8: one per CU)
-  int64_t n_heavy = 0, n_hunits = 0, n_segs = 0;
+  int hot_grid = 0;  // workgroups of k_spmv_hot (a multiple of C: one per CU)
+  int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
+  pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;

@@ -101,10 +101,6 @@ constexpr uint32_t kRowDegMask = (1u << 28) - 1;
 constexpr uint32_t kRowSink = 1u << 28;    // in the dangling set D (contributes to dc)
 constexpr uint32_t kRowIndeg0 = 1u << 29;  // no in-link: the old rank is the sum
 constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
-constexpr uint32_t kRowHeavy = 1u << 31;   // class-split row (its sum comes from the epilogue)
-// Only rows with at least this many in-links are split by class: a split row costs C partial
-// slots (write + read) and C row lengths, worth it only when enough gathers gain L2 locality.
-constexpr int kHeavyMinIndeg = 16;
 
 // ---- heavy rows: wave units with an LDS-resident hot set (pr_spmv.h k_spmv_hot) -------------
 // A wave unit is one wavefront's work: kWavePT in-link entries per lane, kWaveUnit entries in
@@ -136,12 +132,11 @@ constexpr int kHotSlotsDefault = kHotSlotsMax;  // 16382 hot contributions (128 
 struct ClassGeom {
   int C;
   int64_t Q_pad, S_pad;
-  int64_t hcum[kMaxClasses + 1];  // heavy rows in regions < x (heavy rows are a prefix of a region)
-  __host__ __device__ int64_t heavy_to_row(int64_t h) const {
-    int y = 0;
-    while (y + 1 < C && hcum[y + 1] <= h) ++y;
-    return (int64_t)y * Q_pad + (h - hcum[y]);
-  }
+};
+
+// Offsets of the per-class partial-sum arrays (split layout), passed to kernels by value.
+struct PartOff {
+  int64_t o[kMaxClasses + 1];
 };
 
 // Where a class's hot contributions live in the gather space: for every part p, positions

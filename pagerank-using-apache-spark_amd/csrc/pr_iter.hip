@@ -163,7 +163,7 @@ int launch_hot(pr_graph *g, int in) {
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
                      g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->nparts * g->S_pad), g->partial.as<double>(),
-                     g->piece_part.as<double>(), g->n_heavy);
+                     g->poff.as<int64_t>(), g->piece_part.as<double>());
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
@@ -216,18 +216,18 @@ int iter_compute(pr_graph *g) {
                        g->rowinfo.as<uint32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
                        g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
   int64_t n_parts = g->n_units;
-  if (g->C > 1 && g->n_heavy > 0) {  // heavy rows: per-class sums, then the epilogue
-    const int64_t H = g->n_heavy;
+  if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
     if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
-                         g->n_segs, g->seg_row.as<int32_t>(), g->seg_cls.as<int32_t>(), g->seg_p0.as<int32_t>(),
-                         g->piece_part.as<double>(), g->partial.as<double>(), H);
+                         g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
+                         g->partial.as<double>());
     hipLaunchKernelGGL(g->C == kMaxClasses ? k_epilogue<kMaxClasses> : k_epilogue<kClasses>, dim3(g->ep_blocks),
-                       dim3(kThreads), 0, s, H, g->geo,
-                       g->partial.as<double>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
-                       g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->nparts,
-                       (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);
+                       dim3(kThreads), 0, s, g->nblk, g->part_off, g->partial.as<double>(),
+                       g->rmask.as<uint16_t>(), g->cbase.as<int32_t>(),
+                       g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
+                       g->cbuf[in].as<double>(), g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping,
+                       g->unit_part.as<double2>() + g->n_units);
     n_parts += g->ep_blocks;
   }
   PR_HIP(hipGetLastError());

@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
     const int64_t vtx = (int64_t)r0 + k;
     const double rold = (k == t) ? rold0 : r[vtx];
     const uint32_t info = (k == t) ? info0 : rowinfo[vtx];
-    if (info & (kRowHole | kRowHeavy)) continue;
+    if (info & kRowHole) continue;
     const double S = (lrp[k + 1] > lrp[k]) ? rowsum[k] : rold;
     const double rn = affine(S, tdc, teleport, damping);
     r[vtx] = rn;
@@ -400,7 +400,8 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           const uint32_t *__restrict__ hmeta,
                                                           const double *__restrict__ cin, uint32_t cin_bytes,
                                                           double *__restrict__ partial,
-                                                          double *__restrict__ piece_part, int64_t H) {
+                                                          const int64_t *__restrict__ poff,
+                                                          double *__restrict__ piece_part) {
   extern __shared__ double hot[];
   // class x runs on XCD x % 8 (round-robin dispatch: workgroup b on XCD b % 8)
   const int x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
@@ -414,8 +415,9 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   if (threadIdx.x == 0) hot[0] = 0.0;
   __syncthreads();
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)(partial + (int64_t)x * H), 0, (uint32_t)(H * 8), 0x00020000);
+  const int64_t p0 = poff[x];
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(partial + p0), 0, (uint32_t)((poff[x + 1] - p0) * 8), 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int64_t beg = ucum[x], end = ucum[x + 1];
@@ -453,12 +455,11 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   }
 }
 
-// Long (row, class) segments: the sum of their pieces in piece order -> partial[x][row].
-__global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const int32_t *__restrict__ seg_row,
-                                                         const int32_t *__restrict__ seg_cls,
+// Long segments: the sum of their pieces in piece order -> partial[seg_slot[q]].
+__global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const int64_t *__restrict__ seg_slot,
                                                          const int32_t *__restrict__ seg_p0,
                                                          const double *__restrict__ piece_part,
-                                                         double *__restrict__ partial, int64_t R) {
+                                                         double *__restrict__ partial) {
   const int lane = lane_id();
   const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
   for (int64_t q = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); q < n_seg; q += nw) {
@@ -466,36 +467,61 @@ __global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const in
     double acc = 0.0;
     for (int k = lane; k < np; k += kWave) acc = __dadd_rn(acc, piece_part[p0 + k]);
     acc = wave_sum(acc);
-    if (lane == 0) partial[(int64_t)seg_cls[q] * R + seg_row[q]] = acc;
+    if (lane == 0) partial[seg_slot[q]] = acc;
   }
 }
 
-// Epilogue of the split layout over the heavy rows h: S = sum of the C class partials in class
-// order (heavy rows always have in-links), then the fused update of k_spmv_units.
+// Epilogue of the split layout, one wave per 64 consecutive rows: S = the row's class partial
+// sums in class order (row L's class-x slot = cbase[blk][x] + rows of the block before L that
+// have class-x in-links: one ballot), the in-degree-0 quirk, then the fused update of
+// k_spmv_units (r' without FMA, c' = r'/d, dangling and L1 partials).
 template <int C>
-__global__ __launch_bounds__(kThreads) void k_epilogue(int64_t H, ClassGeom geo, const double *__restrict__ partial,
+__global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po, const double *__restrict__ partial,
+                                                       const uint16_t *__restrict__ rmask,
+                                                       const int32_t *__restrict__ cbase,
                                                        const uint32_t *__restrict__ rowinfo,
                                                        double *__restrict__ r, double *__restrict__ cout,
-                                                       const double *__restrict__ cin, int P,
+                                                       const double *__restrict__ cin, int P, int64_t S_pad,
                                                        double n_vertices, double teleport, double damping,
                                                        double2 *__restrict__ ep_part) {
+  typedef int cb_t __attribute__((ext_vector_type(C)));
   __shared__ double2 red2[kThreads / kWave];
-  const double tdc = dc_from_slots(cin, P, geo.S_pad) / n_vertices;
+  const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+  const int lane = lane_id();
   double dcp = 0.0, l1p = 0.0;
-  for (int64_t h = (int64_t)blockIdx.x * kThreads + threadIdx.x; h < H; h += (int64_t)gridDim.x * kThreads) {
-    const int64_t L = geo.heavy_to_row(h);
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  for (int64_t blk = (int64_t)blockIdx.x * (kThreads / kWave) + wv; blk < nblk; blk += nw) {
+    const int64_t L = blk * kWave + lane;  // rows come in whole blocks (holes flagged)
+    const uint32_t m = rmask[L];
     const uint32_t info = rowinfo[L];
     const double rold = r[L];
-    double S = __builtin_nontemporal_load(partial + h);
+    // the block's C first-slot indices in one scalar load (cbase is [blk][C])
+    const cb_t cb = *(const __attribute__((address_space(4))) cb_t *)(cbase + blk * C);
+    // every class's partial load in flight before the first add (absent: out of range, no request)
+    double v[C];
 #pragma unroll
-    for (int x = 1; x < C; ++x) S = __dadd_rn(S, __builtin_nontemporal_load(partial + (int64_t)x * H + h));
-    if (info & kRowIndeg0) S = rold;
+    for (int x = 0; x < C; ++x) {
+      const bool has = (m >> x) & 1u;
+      const unsigned long long bal = __ballot(has);
+      const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(partial + po.o[x]), 0, (uint32_t)((po.o[x + 1] - po.o[x]) * 8), 0x00020000);
+      const uint32_t off = has ? ((uint32_t)cb[x] + (uint32_t)pre) * 8u : 0xFFFFFFF8u;
+      v[x] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(prs, off, 0, 2));
+    }
+    double S = 0.0;
+#pragma unroll
+    for (int x = 0; x < C; ++x) S = __dadd_rn(S, v[x]);  // absent classes add an exact 0
+    if (m == 0) S = rold;  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
     const double rn = affine(S, tdc, teleport, damping);
-    r[L] = rn;
-    const uint32_t d = info & kRowDegMask;
-    if (d > 0) cout[L] = __ddiv_rn(rn, (double)d);
-    else if (info & kRowSink) dcp = __dadd_rn(dcp, rn);
-    l1p = __dadd_rn(l1p, fabs(rn - rold));
+    if (!(info & kRowHole)) {
+      r[L] = rn;
+      const uint32_t d = info & kRowDegMask;
+      if (d > 0) cout[L] = __ddiv_rn(rn, (double)d);
+      else if (info & kRowSink) dcp = __dadd_rn(dcp, rn);
+      l1p = __dadd_rn(l1p, fabs(rn - rold));
+    }
   }
   const double2 part = block_sum2<kThreads>(make_double2(dcp, l1p), red2);
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;

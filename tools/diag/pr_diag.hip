@@ -172,8 +172,8 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   HotGeom hg = g->hot;
   uint32_t *colh = g->colh.as<uint32_t>(), *hmeta = g->hmeta.as<uint32_t>();
   double *cin = g->cbuf[0].as<double>(), *partial = g->partial.as<double>(), *pp = g->piece_part.as<double>();
-  int64_t H = g->n_heavy;
-  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &pp, &H};
+  int64_t *poff = g->poff.as<int64_t>();
+  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &poff, &pp};
   hipEvent_t a, b;
   PR_HIP(hipEventCreate(&a));
   PR_HIP(hipEventCreate(&b));

@@ -45,7 +45,7 @@ def counter_per_pass(d, name):
             continue
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per[(key, kn)] = per.get((key, kn), 0.0) + float(r["Counter_Value"])
-    n_iter = len({k for (k, kn) in per if "k_spmv_units" in kn}) or 1
+    n_iter = len({k for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn}) or 1
     return sum(per.values()) / n_iter if per else None
 
 
