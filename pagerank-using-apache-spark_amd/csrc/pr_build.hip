@@ -371,14 +371,14 @@ __global__ void k_mark_ends(int64_t R, const int64_t *__restrict__ rp, int32_t *
 }
 
 // Row class masks: bit x when the row has a class-x in-link.
-__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, uint16_t *__restrict__ rmask) {
+__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, uint32_t *__restrict__ rmask) {
   for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
     uint32_t m = 0;
     for (int x = 0; x < C; ++x) {
       const int64_t *rp = rp_all + (int64_t)x * (R + 1);
       if (rp[L + 1] > rp[L]) m |= 1u << x;
     }
-    rmask[L] = (uint16_t)m;
+    rmask[L] = m;
   }
 }
 
@@ -447,9 +447,9 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 // Tuning knobs read at build time: column classes of the split layout (8 = one
 // per XCD, 16 = two per XCD) and the size of the LDS hot set.
 static int class_setting() {
-  int c = kMaxClasses;
+  int c = kClasses;
   if (const char *e = getenv("PR_CLASSES")) c = atoi(e);
-  return c == 16 ? 16 : 8;
+  return (c == 8 || c == 32) ? c : 16;
 }
 
 static int hot_slots_setting() {
@@ -459,7 +459,7 @@ static int hot_slots_setting() {
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
-  static_assert(kMaxClasses == 2 * kXcds && kClasses == kXcds, "class counts");
+  static_assert(kMaxClasses == 4 * kXcds && kClasses % kXcds == 0, "class counts");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -682,9 +682,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
-    PR_TRY(g->rmask.alloc(sizeof(uint16_t) * ((size_t)R + 1)));
+    PR_TRY(g->rmask.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
     hipLaunchKernelGGL(k_row_masks, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
-                       g->rmask.as<uint16_t>());
+                       g->rmask.as<uint32_t>());
     PR_HIP(hipGetLastError());
     rp_all.reset();
     if (wp.len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");

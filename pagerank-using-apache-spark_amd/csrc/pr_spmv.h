@@ -393,7 +393,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   }
 }
 
-template <int DEPTH_UNUSED = 0, int DIAG = 0>
+template <int ORDER = 0, int DIAG = 0>
 __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
                                                           const int64_t *__restrict__ ucum, HotGeom hg,
                                                           const uint32_t *__restrict__ colh,
@@ -447,8 +447,13 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
       const int64_t k2 = k + 2 * stride;
       u[s2] = unit_at(k2 < end ? k2 : none_k);
       wave_unit_codes(u[s2], colh, hmeta, k2, wc[s2]);
-      wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
-      wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+      if constexpr (ORDER == 0) {
+        wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
+        wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+      } else {  // reduce first: a gather issue stalled by a busy address unit cannot hold it up
+        wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+        wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
+      }
       k += stride;
       if (k >= end) return;
     }
@@ -477,7 +482,7 @@ __global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const in
 // k_spmv_units (r' without FMA, c' = r'/d, dangling and L1 partials).
 template <int C>
 __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po, const double *__restrict__ partial,
-                                                       const uint16_t *__restrict__ rmask,
+                                                       const uint32_t *__restrict__ rmask,
                                                        const int32_t *__restrict__ cbase,
                                                        const uint32_t *__restrict__ rowinfo,
                                                        double *__restrict__ r, double *__restrict__ cout,

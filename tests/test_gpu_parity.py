@@ -43,7 +43,7 @@ def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, lay
     ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
     with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout) as g:
         if layout != "auto":
-            assert g.info()["classes"] in ((1,) if layout == "fused" else (8, 16))
+            assert g.info()["classes"] in ((1,) if layout == "fused" else (8, 16, 32))
         assert_csr_equal(g, csr)
         hist = []
         ranks, stats = g.run(iters, init_ranks=init, want_ranks_in_callback=True,
@@ -259,6 +259,53 @@ def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef, layout):
     # size-independent property: rank mass bookkeeping. Without no-link keys, the only
     # change of sum(r) per iteration comes from in-degree-0 rows and the dangling term.
     assert np.all(r >= 0.15)
+
+
+@pytest.mark.parametrize("slots", [0, 37, 1000])
+def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
+    """A hot set smaller than the class regions (PR_HOT_SLOTS, read at build time): most entries
+    take k_spmv_hot's gather-space loads instead of the LDS -- the path every large graph uses --
+    with hub segments split into pieces, empty (row, class) pairs and several parts."""
+    monkeypatch.setenv("PR_HOT_SLOTS", str(slots))
+    rng = np.random.default_rng(40 + slots)
+    V = 30000
+    src, dst = random_edges(rng, V, 400000, hub_frac=0.03)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10, layout="split")
+    assert info["n_long_rows"] > 0
+    for it in range(10):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+        assert abs(stats[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout="split")
+             for p in range(3)]
+    try:
+        r = hip.PartGroup(parts).run(10)
+        assert max_rel(r, ref["ranks"]) <= RANK_TOL
+    finally:
+        for p in parts:
+            p.close()
+
+
+def test_rmat_s20_split_default_hot_set(hip, oracle_c):
+    """BASELINE.json configs[0] (R-MAT scale 20, edge factor 16, 10 iterations) at full size
+    through the product layout: 16 classes of ~40 K rows, so the 16 K-slot hot set covers only
+    the top of each class and both gather paths carry real traffic."""
+    import torch
+
+    scale, E = 20, 16 << 20
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    hip.gen_rmat(0, scale, E, s.data_ptr(), d.data_ptr(), seed=1)
+    V = hip.intern_device(0, E, 1 << scale, s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    hs, hd = s.cpu().numpy(), d.cpu().numpy()
+    csr = oracle_c.build_csr(V, hs, hd)
+    ref = oracle_c.run(csr, 10, keep_history=True)
+    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, layout="split") as g:
+        assert g.info()["n_edges"] == csr.n_edges
+        hist = []
+        r, st = g.run(10, want_ranks_in_callback=True, callback=lambda it, rr, ss: hist.append(rr))
+    for it in range(10):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
 @pytest.mark.parametrize("layout", ["fused", "split"])

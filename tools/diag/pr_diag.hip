@@ -94,6 +94,31 @@ __global__ __launch_bounds__(256) void k_gather_bench(const double *__restrict__
   if (acc == 12345.0) out[t] = acc;
 }
 
+// TA-cost probe: every thread issues 8 random 8-byte loads from a table; lane l is active in
+// load j when ((l * 8 + j) * 2654435761u >> 16) % 64 < active (OOB offset otherwise, or
+// exec-masked when MASKED).  Time per instruction vs active lanes separates per-lane from
+// per-instruction address-processing cost.
+template <bool MASKED>
+__global__ __launch_bounds__(256) void k_ta_probe(const double *__restrict__ table, uint32_t n_words, int64_t n_threads,
+                                                  uint32_t seed, int active, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_threads) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, n_words * 8u, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t w = mix32((uint32_t)t * 8u + j + seed) % n_words;
+    const bool on = (int)((((uint32_t)(lane * 8 + j) * 2654435761u) >> 16) % 64u) < active;
+    if constexpr (MASKED) {
+      if (on) acc += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, w * 8u, 0, 0));
+    } else {
+      acc += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, on ? w * 8u : 0xFFFFFFF8u, 0, 0));
+    }
+  }
+  if (acc == 12345.0) out[t] = acc;
+}
+
 extern "C" {
 
 // variant: 0 = PT 8 + nt cols (product), 1 = PT 8 plain cols, 2 = PT 16 + nt, 3 = PT 4 + nt,
@@ -144,12 +169,13 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 
 // Split layout: time the heavy-row kernel k_spmv_hot<0, DIAG> on the graph's own layout.
 // variant = DIAG: 0 = product, 1 = all values from LDS, 2 = no partial stores, 3 = non-temporal
-// partial stores, 4 / 5 = gathers folded into 4 / 32 MiB (1, 2, 4, 5: diagnostics, results wrong).  The hot-set size is a build setting
+// partial stores, 4 / 5 = gathers folded into 4 / 32 MiB (1, 2, 4, 5: diagnostics, results wrong);
+// 13 / 14 / 15 = variants 0 / 1 / 4 with the reduce of unit i before the gathers of i+1.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[13] = {reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[16] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -161,8 +187,11 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 9>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 10>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 11>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 12>)};
-  if (variant < 0 || variant > 12 || variant == 7) return fail(PR_ERR_INVALID, "unknown variant");
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 12>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 0>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 4>)};
+  if (variant < 0 || variant > 15 || variant == 7) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -219,6 +248,40 @@ int prd_gather_bench(int device, int64_t table_bytes, int64_t n_loads, int mode,
         case 3: hipLaunchKernelGGL(k_gather_bench<17>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
         default: hipLaunchKernelGGL(k_gather_bench<0>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, seed, (double *)out); break;
       }
+    }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
+  return PR_OK;
+}
+
+
+// TA probe (see k_ta_probe): n_loads = 8 * threads; returns ms per launch.
+int prd_ta_probe(int device, int64_t table_bytes, int64_t n_loads, int active, int masked, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  void *tab = nullptr, *out = nullptr;
+  PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8));
+  const int64_t nt = n_loads / 8;
+  const uint32_t nw = (uint32_t)(table_bytes / 8);
+  const dim3 grid((unsigned)((nt + 255) / 256));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i) {
+      if (masked) hipLaunchKernelGGL(k_ta_probe<true>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
+      else hipLaunchKernelGGL(k_ta_probe<false>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
     }
     PR_HIP(hipGetLastError());
     PR_HIP(hipEventRecord(b, 0));
