@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 METRIC = "PageRank GTEPS/iter + % HBM roofline, R-MAT scale-26 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 # bumped whenever the SpMV pass changes, so a stale rocprof traffic figure is never reported
-LAYOUT_VERSION = "hot-wave-v1"
+LAYOUT_VERSION = "masked-split-v1"
 
 
 def log(msg: str) -> None:
@@ -160,8 +160,8 @@ def main() -> int:
     n_edges = info["n_edges"]
     gteps = n_edges / (ms_step * 1e-3) / 1e9
 
-    # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot for class-split heavy
-    # rows, k_spmv_units for light rows, k_seg_reduce + k_epilogue) -- on this rank
+    # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot per column class,
+    # k_seg_reduce for long segments, k_epilogue over all rows) -- on this rank
     spmv_ms = st["spmv_ms_mean"]
     bytes_launch = 12 * info["local_edges"] + 36 * info["local_rows"]
     achieved = bytes_launch / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
@@ -203,7 +203,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(workload) if world == 1 else None,
-                "kernel": "spmv pass: k_spmv_hot (heavy rows) + k_spmv_units (light rows) + k_seg_reduce + k_epilogue",
+                "kernel": "spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue (split layout, 16 column classes)",
                 "classes": info.get("classes"),
                 "bytes_model": "12*E'_part + 36*V_part per launch (pull-fp64-v1)",
                 "spmv_ms_mean": round(spmv_ms, 4),
