@@ -1,6 +1,6 @@
 """Benchmark: PageRank GTEPS per iteration + % of HBM roofline on R-MAT scale-26 (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 26] [--graph rmat|er]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 26] [--graph rmat|er|lj|twitter]
 
 A step is one PageRank iteration (Sparky.java:189-235) over the whole graph, inputs resident
 in HBM.  The graph is generated on the GPU (seeded R-MAT, Graph500 a/b/c = .57/.19/.19,
@@ -86,7 +86,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edge-factor", type=int, default=16)
-    ap.add_argument("--graph", choices=["rmat", "er"], default="rmat")
+    ap.add_argument("--graph", choices=["rmat", "er", "lj", "twitter"], default="rmat",
+                    help="lj / twitter: the Chung-Lu shapes of BASELINE.json configs[1] / [4]")
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
@@ -110,18 +111,32 @@ def main() -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
 
-    seed = a.seed if a.seed is not None else (2 if a.graph == "rmat" else 3)
-    E = a.edge_factor << a.scale
     t0 = time.perf_counter()
+    if a.graph in ("rmat", "er"):
+        seed = a.seed if a.seed is not None else (2 if a.graph == "rmat" else 3)
+        E = a.edge_factor << a.scale
+        labels = 1 << a.scale
+    else:
+        pre = dict(sparky_hip.CHUNGLU_PRESETS[a.graph])
+        seed = a.seed if a.seed is not None else pre["seed"]
+        E = pre["n_edges"] + pre["n_nolink"]
+        labels = pre["n_labels"]
     s = torch.empty(E, dtype=torch.int32, device="cuda")
     d = torch.empty(E, dtype=torch.int32, device="cuda")
     if a.graph == "rmat":
         sparky_hip.gen_rmat(dev, a.scale, E, s.data_ptr(), d.data_ptr(), seed=seed)
         workload = f"R-MAT scale-{a.scale} edge-factor {a.edge_factor} (Graph500 .57/.19/.19, seed {seed})"
-    else:
+    elif a.graph == "er":
         sparky_hip.gen_er(dev, a.scale, E, s.data_ptr(), d.data_ptr(), seed=seed)
         workload = f"Erdos-Renyi scale-{a.scale} degree {a.edge_factor} (seed {seed})"
-    V = sparky_hip.intern_device(dev, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    else:
+        sparky_hip.gen_chunglu(dev, pre["n_labels"], pre["n_edges"], s.data_ptr(), d.data_ptr(),
+                               gamma_out=pre["gamma_out"], v0_out=pre["v0_out"], gamma_in=pre["gamma_in"],
+                               v0_in=pre["v0_in"], src_frac=pre["src_frac"], n_nolink=pre["n_nolink"], seed=seed)
+        workload = (f"{'LiveJournal' if a.graph == 'lj' else 'Twitter-2010'}-shaped Chung-Lu "
+                    f"({pre['n_labels']} labels, {pre['n_edges']} edges + {pre['n_nolink']} link-less records, "
+                    f"gamma out/in {pre['gamma_out']}/{pre['gamma_in']}, seed {seed})")
+    V = sparky_hip.intern_device(dev, E, labels, s.data_ptr(), d.data_ptr())
     t_gen = time.perf_counter() - t0
     log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
     want_cpu = (rank == 0 and world == 1 and not a.no_cpu_baseline)

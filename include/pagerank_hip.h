@@ -157,6 +157,15 @@ int pr_gen_rmat(int32_t device, int32_t scale, int64_t n_edges, double a, double
 /* Uniform Erdos-Renyi G(n, m): src, dst uniform over 2^scale labels. */
 int pr_gen_er(int32_t device, int32_t scale, int64_t n_edges, uint64_t seed, int32_t *d_src,
               int32_t *d_dst);
+/* Chung-Lu graph with power-law weights (the LiveJournal- and Twitter-shaped
+ * configs): n_edges edges whose source rank follows w(r) ~ (r + v0_out)^(-1/(gamma_out-1)) over
+ * ranks [0, src_frac * n_labels) and whose target rank follows the same law with gamma_in, v0_in
+ * over [0, n_labels); then n_nolink records (label, -1) for the ranks just past the source range
+ * (keys without links).  Ranks map to labels by a seeded bijection of [0, n_labels).
+ * d_src/d_dst: device arrays of n_edges + n_nolink int32. */
+int pr_gen_chunglu(int32_t device, int32_t n_labels, int64_t n_edges, double gamma_out, double v0_out,
+                   double gamma_in, double v0_in, double src_frac, int64_t n_nolink, uint64_t seed,
+                   int32_t *d_src, int32_t *d_dst);
 /* Relabel raw labels in [0, label_bound) to dense IDs in first-appearance order (src before
  * dst, edge by edge) -- the same mapping the host URL interner produces -- in place.
  * dst == -1 entries are kept.  *n_vertices_out = number of distinct labels. */

@@ -5,12 +5,21 @@
 // whole front-end on the GPU: a counter-based R-MAT / Erdos-Renyi generator writes raw labels,
 // and pr_intern_device relabels them in first-appearance order -- the exact mapping the host
 // interner would produce for the same edge list written as text.
+#include <cmath>
+
 #include "pr_compact.h"
 #include "pr_device.h"
 #include "pr_internal.h"
 
 namespace pr {
 namespace {
+
+inline uint64_t splitmix64_host(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -67,6 +76,41 @@ __global__ void k_gen_er(int scale, int64_t E, uint64_t seed, int32_t *__restric
     const uint64_t h = edge_hash(seed, (uint64_t)i, 0);
     src[i] = (int32_t)((uint32_t)h & mask);
     dst[i] = (int32_t)((uint32_t)(h >> 32) & mask);
+  }
+}
+
+// Chung-Lu: endpoint ranks drawn from a truncated continuous power law w(r) ~ (r + v0)^-beta by
+// inverse transform, then labels = (rank * mul + add) mod n_labels (a bijection: gcd(mul, n) = 1).
+// Sources use ranks [0, n_src), so ranks >= n_src never send a link (sink-only vertices); records
+// E .. E + n_nolink - 1 are "(url, null)" lines for ranks n_src .. n_src + n_nolink - 1 (keys
+// without links, Sparky.java:114-118).
+struct PowerLaw {
+  double a, lo, span, v0;  // a = 1 - beta; lo = v0^a; span = (n + v0)^a - v0^a
+  int64_t n;
+};
+
+__device__ __forceinline__ int64_t power_rank(const PowerLaw &pl, uint64_t h) {
+  const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  const double x = pow(pl.lo + u * pl.span, 1.0 / pl.a) - pl.v0;
+  int64_t r = (int64_t)x;
+  r = r < 0 ? 0 : r;
+  return r >= pl.n ? pl.n - 1 : r;
+}
+
+__global__ void k_gen_chunglu(int64_t E, int64_t n_nolink, int64_t n_labels, PowerLaw out, PowerLaw in,
+                              uint64_t mul, uint64_t add, uint64_t seed, int32_t *__restrict__ src,
+                              int32_t *__restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < E + n_nolink;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t rs, rd = -1;
+    if (i < E) {
+      rs = power_rank(out, edge_hash(seed, (uint64_t)i, 0));
+      rd = power_rank(in, edge_hash(seed, (uint64_t)i, 1));
+    } else {
+      rs = out.n + (i - E);
+    }
+    src[i] = (int32_t)(((uint64_t)rs * mul + add) % (uint64_t)n_labels);
+    dst[i] = rd < 0 ? -1 : (int32_t)(((uint64_t)rd * mul + add) % (uint64_t)n_labels);
   }
 }
 
@@ -168,6 +212,42 @@ int pr_gen_er(int32_t device, int32_t scale, int64_t n_edges, uint64_t seed, int
   if (n_edges > 0)
     hipLaunchKernelGGL(k_gen_er, dim3(grid_for(n_edges, 256, 65536)), dim3(256), 0, 0, scale,
                        n_edges, seed, d_src, d_dst);
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipDeviceSynchronize());
+  return PR_OK;
+}
+
+int pr_gen_chunglu(int32_t device, int32_t n_labels, int64_t n_edges, double gamma_out, double v0_out,
+                   double gamma_in, double v0_in, double src_frac, int64_t n_nolink, uint64_t seed,
+                   int32_t *d_src, int32_t *d_dst) {
+  PR_TRY(gen_check(device, 1, n_edges + n_nolink, d_src, d_dst));
+  if (n_labels < 1) return fail(PR_ERR_INVALID, "n_labels must be >= 1");
+  if (!(gamma_out > 1.0 && gamma_in > 1.0 && gamma_out != 2.0 && gamma_in != 2.0))
+    return fail(PR_ERR_INVALID, "power-law exponents must be > 1 and != 2");
+  if (!(v0_out > 0.0 && v0_in > 0.0)) return fail(PR_ERR_INVALID, "v0 must be > 0");
+  const int64_t n_src = (int64_t)(src_frac * (double)n_labels);
+  if (n_src < 1 || n_nolink < 0 || n_src + n_nolink > n_labels)
+    return fail(PR_ERR_INVALID, "src_frac * n_labels + n_nolink must fit in [1, n_labels]");
+  auto law = [](double gamma, double v0, int64_t n) {
+    PowerLaw p{};
+    p.a = 1.0 - 1.0 / (gamma - 1.0);
+    p.v0 = v0;
+    p.lo = std::pow(v0, p.a);
+    p.span = std::pow((double)n + v0, p.a) - p.lo;
+    p.n = n;
+    return p;
+  };
+  const PowerLaw out = law(gamma_out, v0_out, n_src), in = law(gamma_in, v0_in, n_labels);
+  auto gcd = [](uint64_t x, uint64_t y) {
+    while (y) { const uint64_t t = x % y; x = y; y = t; }
+    return x;
+  };
+  uint64_t mul = (splitmix64_host(seed + 23) % (uint64_t)n_labels) | 1u, add = splitmix64_host(seed + 29) % (uint64_t)n_labels;
+  while (gcd(mul, (uint64_t)n_labels) != 1) mul += 2;
+  DevScope ds(device);
+  if (n_edges + n_nolink > 0)
+    hipLaunchKernelGGL(k_gen_chunglu, dim3(grid_for(n_edges + n_nolink, 256, 65536)), dim3(256), 0, 0, n_edges,
+                       n_nolink, (int64_t)n_labels, out, in, mul, add, seed, d_src, d_dst);
   PR_HIP(hipGetLastError());
   PR_HIP(hipDeviceSynchronize());
   return PR_OK;

@@ -43,7 +43,7 @@ EXPORTED = [
     "pr_abi_version", "pr_last_error", "pr_device_count", "pr_graph_create", "pr_graph_create_part",
     "pr_graph_info", "pr_graph_export_csr", "pr_run", "pr_reset", "pr_step", "pr_sync",
     "pr_get_ranks", "pr_set_timing", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
-    "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_intern_device", "pr_group_reset",
+    "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_gen_chunglu", "pr_intern_device", "pr_group_reset",
     "pr_group_step", "pr_group_sync",
 ]
 
@@ -103,6 +103,7 @@ def load() -> ctypes.CDLL:
         "pr_graph_destroy": ([P], None),
         "pr_gen_rmat": ([i32, i32, i64, dbl, dbl, dbl, u64, P, P], ctypes.c_int),
         "pr_gen_er": ([i32, i32, i64, u64, P, P], ctypes.c_int),
+        "pr_gen_chunglu": ([i32, i32, i64, dbl, dbl, dbl, dbl, dbl, i64, u64, P, P], ctypes.c_int),
         "pr_intern_device": ([i32, i64, i32, P, P, P], ctypes.c_int),
         "pr_group_reset": ([P, i32, dbl, dbl, P], ctypes.c_int),
         "pr_group_step": ([P, i32, i32], ctypes.c_int),

@@ -193,6 +193,24 @@ def gen_rmat(device: int, scale: int, n_edges: int, src_ptr: int, dst_ptr: int, 
                                   ctypes.c_void_p(dst_ptr)))
 
 
+# Chung-Lu shapes of BASELINE.json's configs: labels, edges, (gamma, v0) of the
+# source and target laws, fraction of ranks that send links, "(url, null)" records, seed.
+CHUNGLU_PRESETS = {
+    "lj": dict(n_labels=4_847_571, n_edges=68_993_773, gamma_out=2.3, v0_out=84.0, gamma_in=2.3, v0_in=84.0,
+               src_frac=1.0, n_nolink=0, seed=4),
+    "twitter": dict(n_labels=41_652_230, n_edges=1_468_365_182, gamma_out=2.2, v0_out=100.0, gamma_in=2.1,
+                    v0_in=50.0, src_frac=0.85, n_nolink=2_082_611, seed=5),
+}
+
+
+def gen_chunglu(device: int, n_labels: int, n_edges: int, src_ptr: int, dst_ptr: int, *, gamma_out: float,
+                v0_out: float, gamma_in: float, v0_in: float, src_frac: float = 1.0, n_nolink: int = 0,
+                seed: int = 4) -> None:
+    """Device arrays of n_edges + n_nolink int32 (pr_gen_chunglu)."""
+    check(_lib.load().pr_gen_chunglu(device, n_labels, n_edges, gamma_out, v0_out, gamma_in, v0_in, src_frac,
+                                     n_nolink, seed, ctypes.c_void_p(src_ptr), ctypes.c_void_p(dst_ptr)))
+
+
 def gen_er(device: int, scale: int, n_edges: int, src_ptr: int, dst_ptr: int, *, seed: int = 3) -> None:
     check(_lib.load().pr_gen_er(device, scale, n_edges, seed, ctypes.c_void_p(src_ptr),
                                 ctypes.c_void_p(dst_ptr)))

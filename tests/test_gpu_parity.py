@@ -309,6 +309,61 @@ def test_rmat_s20_split_default_hot_set(hip, oracle_c):
 
 
 @pytest.mark.parametrize("layout", ["fused", "split"])
+def test_chunglu_generator_small(hip, oracle_c, layout):
+    """The Chung-Lu generator (LJ / Twitter shapes) on a small instance with sink-only ranks and
+    link-less records: raw labels in range, the link-less records present, interning equal to the
+    host's, graph and ranks equal to the oracle's."""
+    import torch
+
+    n_labels, E, nolink = 30011, 400000, 1500
+    s = torch.empty(E + nolink, dtype=torch.int32, device="cuda")
+    d = torch.empty(E + nolink, dtype=torch.int32, device="cuda")
+    hip.gen_chunglu(0, n_labels, E, s.data_ptr(), d.data_ptr(), gamma_out=2.2, v0_out=20.0, gamma_in=2.1,
+                    v0_in=10.0, src_frac=0.85, n_nolink=nolink, seed=5)
+    torch.cuda.synchronize()
+    raw_s, raw_d = s.cpu().numpy(), d.cpu().numpy()
+    assert raw_s.min() >= 0 and raw_s.max() < n_labels and raw_d.max() < n_labels
+    assert np.all(raw_d[E:] == -1) and np.all(raw_d[:E] >= 0)
+    indeg = np.bincount(raw_d[:E], minlength=n_labels)
+    assert indeg.max() > 50 * indeg[indeg > 0].mean()  # power-law head
+    V = hip.intern_device(0, E + nolink, n_labels, s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    Vh, hs, hd = host_first_appearance(raw_s, raw_d)
+    assert V == Vh and np.array_equal(s.cpu().numpy(), hs) and np.array_equal(d.cpu().numpy(), hd)
+    csr = oracle_c.build_csr(V, hs, hd)
+    ref = oracle_c.run(csr, 10)
+    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E + nolink,
+                           layout=layout) as g:
+        assert_csr_equal(g, csr)
+        info = g.info()
+        r, st = g.run(10)
+    assert info["n_nolink"] > 0 and info["n_sink"] > 0.05 * V
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+
+
+def test_lj_shaped_full_size(hip, oracle_c):
+    """BASELINE.json configs[1]: the LiveJournal-shaped Chung-Lu graph (4.85 M labels, 69 M edges),
+    20 iterations, product layout, against the oracle."""
+    import torch
+
+    pre = dict(hip.CHUNGLU_PRESETS["lj"])
+    E = pre["n_edges"] + pre["n_nolink"]
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    hip.gen_chunglu(0, pre["n_labels"], pre["n_edges"], s.data_ptr(), d.data_ptr(), gamma_out=pre["gamma_out"],
+                    v0_out=pre["v0_out"], gamma_in=pre["gamma_in"], v0_in=pre["v0_in"], src_frac=pre["src_frac"],
+                    n_nolink=pre["n_nolink"], seed=pre["seed"])
+    V = hip.intern_device(0, E, pre["n_labels"], s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+    csr = oracle_c.build_csr(V, s.cpu().numpy(), d.cpu().numpy())
+    ref = oracle_c.run(csr, 20)
+    with hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E) as g:
+        assert g.info()["n_edges"] == csr.n_edges and g.info()["classes"] > 1
+        r, st = g.run(20)
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+
+
+@pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("P", [2, 3, 4])
 def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout):
     """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
