@@ -151,6 +151,9 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         g.attach_comm(rank, world, obj[0])
 
+    xchg_desc = (" + RCCL all-gather of whole slices" if os.environ.get("PR_EXCHANGE") == "allgather"
+                 else " + RCCL grouped send/recv of the needed contributions")
+
     g.reset()
     g.step(a.warmup)
     g.sync()
@@ -208,7 +211,8 @@ def main() -> int:
                 "n_vertices": V,
                 "n_edges_raw": E,
                 "n_edges_dedup": n_edges,
-                "parallelism": f"row-partition x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"row-partition x{world}" + (xchg_desc if world > 1 else ""),
+                "exchange_doubles_per_iter_rank0": info.get("xchg_send", 0) if world > 1 else 0,
                 "iterations_timed": a.steps,
             },
             "roofline": {

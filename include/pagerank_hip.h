@@ -66,7 +66,9 @@ extern "C" {
 #define PR_INFO_N_LONG_ROWS 11 /* rows split across several units                          */
 #define PR_INFO_DEVICE_BYTES 12
 #define PR_INFO_CLASSES 13     /* column classes of the layout (1 = fused single pass)     */
-#define PR_INFO_COUNT 14
+#define PR_INFO_XCHG_SEND 14   /* doubles this part sends per iteration (P > 1)           */
+#define PR_INFO_XCHG_RECV 15   /* doubles this part receives per iteration (P > 1)        */
+#define PR_INFO_COUNT 16
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

@@ -39,26 +39,13 @@ void DevBuf::reset() {
   bytes = 0;
 }
 
-// All-gather of the contribution slices (+ the two slots) across parts: the only data
-// exchange of the row-partitioned iteration.  In place: part p's slice is
-// already at offset p * S_pad of the buffer.
-int exchange(pr_graph *g, int buf) {
-  if (g->nparts <= 1) return PR_OK;
-  if (!g->comm) return fail(PR_ERR_STATE, "graph part has no communicator (pr_graph_attach_comm)");
-  double *base = g->cbuf[buf].as<double>();
-  ncclResult_t rc = ncclAllGather(base + (int64_t)g->part * g->S_pad, base, (size_t)g->S_pad,
-                                  ncclDouble, g->comm, g->stream);
-  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
-  return PR_OK;
-}
-
 }  // namespace pr
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
   b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
-  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes;
+  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_recv.bytes + x_sbuf.bytes + x_rbuf.bytes;
   return b;
 }
 
@@ -153,11 +140,20 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
   return create_common(device, part, n_parts, n_vertices, n_edges, src, dst, flags, out);
 }
 
+// doubles moved per iteration by this part: the packed runs, or whole slices (PR_EXCHANGE=allgather)
+static int64_t xchg_volume(const pr_graph *g, bool send) {
+  if (g->nparts <= 1) return 0;
+  if (g->x_allgather) return (send ? 1 : g->nparts - 1) * g->S_pad;
+  const std::vector<int64_t> &o = send ? g->x_soff : g->x_roff;
+  return o.empty() ? 0 : o.back();
+}
+
 int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
-                                    g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C};
+                                    g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C,
+                                    xchg_volume(g, true), xchg_volume(g, false)};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }
@@ -318,6 +314,14 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
   }
   g->comm_rank = rank;
   g->comm_size = n_ranks;
+  if (n_ranks > 1) {
+    const int rv = pr::verify_exchange(g);
+    if (rv != PR_OK) {
+      ncclCommDestroy(g->comm);
+      g->comm = nullptr;
+      return rv;
+    }
+  }
   return PR_OK;
 }
 

@@ -550,9 +550,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   g->n_local_max = (V + P - 1) / P;
   g->n_local = V > part ? (V - part + P - 1) / P : 0;
   if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
-  // Column classes: one per XCD when the part's contribution slice outgrows the L2s (pr_graph.h).
+  // Column classes when the gather space (every part's slice: the columns a part reads) outgrows
+  // the L2s (pr_graph.h).
   const int c_split = class_setting();
-  int C = (g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
+  int C = ((int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
   if (g->flags & PR_LAYOUT_SPLIT) C = c_split;
   // heavy-row entry codes are byte offsets below 2^31 (pr_internal.h)
@@ -584,6 +585,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   geo.Q_pad = g->Q_pad;
   geo.S_pad = g->S_pad;
   g->geo = geo;
+
+  // ---- exchange lists (P > 1): which of this part's contributions every peer reads ----
+  PR_TRY(build_exchange(g, ukeys, m, b, maskb, rank_of.as<int32_t>(), gpos.as<int32_t>()));
 
   // ---- the part's in-link CSRs: one per column class (one in the fused layout) ----
   const int64_t R = g->n_rows;

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact_write(int64_t n, in
   }
 }
 
-// Returns the number of selected items in *count (host).  `out` must have room for them.
+// Returns the number of selected items in *count (host).  `out` must have room for them;
+// out == nullptr only counts.
 template <class Pred, class Xform, class OutT>
 int compact_index(int64_t n, Pred pred, Xform xf, OutT *out, int64_t *count, hipStream_t s) {
   *count = 0;
@@ -79,6 +80,10 @@ int compact_index(int64_t n, Pred pred, Xform xf, OutT *out, int64_t *count, hip
   PR_HIP(hipStreamSynchronize(s));
   int64_t acc = 0;
   for (int w = 0; w < nwg; ++w) { ho[w] = acc; acc += hc[w]; }
+  if (out == nullptr) {  // count only
+    *count = acc;
+    return PR_OK;
+  }
   PR_HIP(hipMemcpyAsync(offs.p, ho.data(), sizeof(int64_t) * nwg, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL((k_compact_write<Pred, Xform, OutT>), dim3(nwg), dim3(kCompactThreads), 0, s,
                      n, tpw, pred, xf, offs.as<int64_t>(), out);

@@ -1,0 +1,306 @@
+// The exchange of the row-partitioned iteration: after its epilogue every part
+// has fresh contributions c' = r'/d for its own rows (its slice of the gather space) and the two
+// slots {dangling partial, L1 partial}.  Part q only ever reads the contributions of the sources
+// of its own in-links, so part p sends q exactly those positions of its slice (plus the two
+// slots), packed densely; q scatters them to their native positions in its copy of the gather
+// space.  Codes, hot sets and kernels are unchanged: positions q never reads stay stale.
+//
+// Both ends derive the p -> q position list from the same edge list with the same rules, so they
+// agree on every count without communicating.  At R-MAT s26 with 8 parts this moves 47 % of the
+// sources an all-gather of whole slices would (and none of the sinks).
+//
+// Transport: RCCL grouped ncclSend / ncclRecv (one process per GPU), or device-to-device copies
+// (pr_group_*: one process, several parts).  PR_EXCHANGE=allgather restores the whole-slice
+// all-gather (A/B, diagnostics).
+#include <cstdlib>
+#include <cstring>
+
+#include "pr_compact.h"
+#include "pr_device.h"
+#include "pr_graph.h"
+
+namespace pr {
+namespace {
+
+// edge (u -> v) of the deduped, sorted edge keys: ((v << b) | u)
+struct XPred {
+  const uint64_t *k;
+  const int32_t *rank_of;
+  int b, P, part;
+  uint64_t mask;
+  bool send;  // send: u owned here, v elsewhere; receive: v owned here, u elsewhere
+  __device__ bool operator()(int64_t i) const {
+    const uint64_t key = k[i];
+    const int pu = rank_of[(int32_t)(key & mask)] % P, pv = rank_of[(int32_t)(key >> b)] % P;
+    return send ? (pu == part && pv != part) : (pv == part && pu != part);
+  }
+};
+// (peer << 32) | position of u inside its owner's slice
+struct XKey {
+  const uint64_t *k;
+  const int32_t *rank_of, *gpos;
+  int b, P;
+  uint64_t mask;
+  int64_t S_pad;
+  bool send;
+  __device__ uint64_t operator()(int64_t i) const {
+    const uint64_t key = k[i];
+    const int32_t u = (int32_t)(key & mask), v = (int32_t)(key >> b);
+    const int64_t gu = gpos[u];
+    const int pu = rank_of[u] % P, pv = rank_of[v] % P;
+    const uint64_t peer = (uint64_t)(send ? pv : pu);
+    return (peer << 32) | (uint64_t)(gu - (int64_t)pu * S_pad);
+  }
+};
+struct XUnique {
+  const uint64_t *k;
+  __device__ bool operator()(int64_t i) const { return i == 0 || k[i] != k[i - 1]; }
+};
+struct XIdent {
+  const uint64_t *k;
+  __device__ uint64_t operator()(int64_t i) const { return k[i]; }
+};
+
+// Sorted unique (peer, pos) keys -> absolute positions grouped by peer (peer order), each peer's
+// run followed by its two slot positions: out[k + 2 * peer_ordinal] for key k.
+__global__ void k_xlist(int64_t n, const uint64_t *__restrict__ keys, const int64_t *__restrict__ first,
+                        int P, int self, int64_t S_pad, bool send, uint32_t *__restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(keys[i] >> 32);
+    const int ord = q - (q > self ? 1 : 0);
+    const int64_t owner = send ? self : q;
+    out[i + 2 * ord] = (uint32_t)(owner * S_pad + (int64_t)(keys[i] & 0xFFFFFFFFull));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < P) {  // the slots close every peer's run
+    const int q = threadIdx.x;
+    if (q != self) {
+      const int ord = q - (q > self ? 1 : 0);
+      const int64_t owner = send ? self : q;
+      const int64_t end = first[q + 1] + 2 * ord;  // run end of peer q
+      out[end] = (uint32_t)(owner * S_pad + S_pad - 2);
+      out[end + 1] = (uint32_t)(owner * S_pad + S_pad - 1);
+    }
+  }
+}
+
+// first[q] = first key of peer >= q (keys sorted by peer)
+__global__ void k_peer_bounds(const uint64_t *__restrict__ keys, int64_t m, int P, int64_t *__restrict__ first) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t qc = (i < m) ? (int64_t)(keys[i] >> 32) : P;
+    const int64_t qp = (i > 0) ? (int64_t)(keys[i - 1] >> 32) : -1;
+    for (int64_t q = qp + 1; q <= qc; ++q) first[q] = i;
+  }
+}
+
+// Four positions per thread (one 16-byte load of the list): the gather/scatter side is the
+// cost, so keep every lane's four loads in flight at once.
+__global__ __launch_bounds__(256) void k_pack(int64_t n, const uint32_t *__restrict__ pos,
+                                              const double *__restrict__ cbuf, double *__restrict__ out) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 p = reinterpret_cast<const uint4 *>(pos)[i];
+    const double a = cbuf[p.x], b = cbuf[p.y], c = cbuf[p.z], d = cbuf[p.w];
+    reinterpret_cast<double2 *>(out)[2 * i] = make_double2(a, b);
+    reinterpret_cast<double2 *>(out)[2 * i + 1] = make_double2(c, d);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    out[i] = cbuf[pos[i]];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack(int64_t n, const uint32_t *__restrict__ pos,
+                                                const double *__restrict__ in, double *__restrict__ cbuf) {
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 p = reinterpret_cast<const uint4 *>(pos)[i];
+    const double2 ab = reinterpret_cast<const double2 *>(in)[2 * i];
+    const double2 cd = reinterpret_cast<const double2 *>(in)[2 * i + 1];
+    cbuf[p.x] = ab.x;
+    cbuf[p.y] = ab.y;
+    cbuf[p.z] = cd.x;
+    cbuf[p.w] = cd.y;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    cbuf[pos[i]] = in[i];
+  }
+}
+
+bool allgather_requested() {
+  const char *e = getenv("PR_EXCHANGE");
+  return e && std::strcmp(e, "allgather") == 0;
+}
+
+// One direction's list (send or receive) of part g->part.
+int build_list(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
+               const int32_t *gpos, bool send, DevBuf *list, std::vector<int64_t> *off) {
+  hipStream_t s = g->stream;
+  const int P = g->nparts, self = g->part;
+  const XPred pred{ukeys, rank_of, b, P, self, mask, send};
+  int64_t n = 0;
+  PR_TRY(compact_index(m, pred, XIdent{ukeys}, (uint64_t *)nullptr, &n, s));  // count only
+  DevBuf keys, tmp, uk, first;
+  PR_TRY(keys.alloc(sizeof(uint64_t) * (n > 0 ? n : 1)));
+  PR_TRY(tmp.alloc(sizeof(uint64_t) * (n > 0 ? n : 1)));
+  int64_t n2 = 0;
+  PR_TRY(compact_index(m, pred, XKey{ukeys, rank_of, gpos, b, P, mask, g->S_pad, send}, keys.as<uint64_t>(), &n2, s));
+  PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), n2, 0, 32 + bits_for((uint64_t)P), s));
+  int64_t nu = 0;
+  PR_TRY(compact_index(n2, XUnique{keys.as<uint64_t>()}, XIdent{keys.as<uint64_t>()}, tmp.as<uint64_t>(), &nu, s));
+  PR_TRY(first.alloc(sizeof(int64_t) * (P + 1)));
+  hipLaunchKernelGGL(k_peer_bounds, dim3(grid_for(nu + 1, 256, 65536)), dim3(256), 0, s, tmp.as<uint64_t>(), nu, P,
+                     first.as<int64_t>());
+  std::vector<int64_t> hf(P + 1);
+  PR_HIP(hipMemcpyAsync(hf.data(), first.p, sizeof(int64_t) * (P + 1), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  const int64_t total = nu + 2 * (P - 1);
+  PR_TRY(list->alloc(sizeof(uint32_t) * (size_t)total));
+  hipLaunchKernelGGL(k_xlist, dim3(grid_for(nu > 0 ? nu : 1, 256, 65536)), dim3(256), 0, s, nu, tmp.as<uint64_t>(),
+                     first.as<int64_t>(), P, self, g->S_pad, send, list->as<uint32_t>());
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipStreamSynchronize(s));
+  off->assign(P + 1, 0);  // offsets of every peer's run (self: empty)
+  for (int q = 0; q < P; ++q) (*off)[q + 1] = (*off)[q] + (q == self ? 0 : (hf[q + 1] - hf[q]) + 2);
+  return PR_OK;
+}
+
+}  // namespace
+
+// doubles per send buffer, even so that the second buffer stays 16-byte aligned (k_pack)
+int64_t send_stride(const pr_graph *g) {
+  const int64_t n = g->x_soff[g->nparts];
+  return (n + 1) & ~int64_t(1);
+}
+
+double *send_runs(const pr_graph *g, int buf) {
+  return g->x_sbuf.as<double>() + (buf & 1) * send_stride(g);
+}
+
+int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
+                   const int32_t *gpos) {
+  g->x_allgather = allgather_requested();
+  if (g->nparts <= 1 || g->x_allgather) return PR_OK;
+  PR_TRY(build_list(g, ukeys, m, b, mask, rank_of, gpos, true, &g->x_send, &g->x_soff));
+  PR_TRY(build_list(g, ukeys, m, b, mask, rank_of, gpos, false, &g->x_recv, &g->x_roff));
+  const int P = g->nparts;
+  // two send buffers, one per gather-space buffer: in the group path a peer's copy out of the
+  // runs of iteration k may still be pending when this part packs iteration k + 1
+  PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
+  PR_TRY(g->x_rbuf.alloc(sizeof(double) * (size_t)(g->x_roff[P] > 0 ? g->x_roff[P] : 1)));
+  return PR_OK;
+}
+
+int exchange_pack(pr_graph *g, int buf) {
+  const int64_t n = g->x_soff[g->nparts];
+  if (n > 0)
+    hipLaunchKernelGGL(k_pack, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, g->stream, n, g->x_send.as<uint32_t>(),
+                       g->cbuf[buf].as<double>(), send_runs(g, buf));
+  PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+
+int exchange_unpack(pr_graph *g, int buf) {
+  const int64_t n = g->x_roff[g->nparts];
+  if (n > 0)
+    hipLaunchKernelGGL(k_unpack, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, g->stream, n, g->x_recv.as<uint32_t>(),
+                       g->x_rbuf.as<double>(), g->cbuf[buf].as<double>());
+  PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+
+// After ncclCommInitRank: every rank publishes {graph shape, exchange mode, its send-run lengths}
+// and checks that what each peer sends it is exactly what it expects to receive, so a mismatch
+// (different inputs, different PR_EXCHANGE per rank) fails loudly at attach time instead of
+// desynchronising the send/receive pairs.
+int verify_exchange(pr_graph *g) {
+  const int P = g->nparts;
+  const int W = P + 3;
+  std::vector<int64_t> mine(W, 0);
+  mine[0] = g->V;
+  mine[1] = g->S_pad;
+  mine[2] = g->x_allgather ? 1 : 0;
+  if (!g->x_allgather)
+    for (int q = 0; q < P; ++q) mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
+  DevBuf d;
+  PR_TRY(d.alloc(sizeof(int64_t) * (size_t)W * (P + 1)));
+  PR_HIP(hipMemcpyAsync(d.as<int64_t>(), mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, g->stream));
+  ncclResult_t rc = ncclAllGather(d.as<int64_t>(), d.as<int64_t>() + W, (size_t)W, ncclInt64, g->comm, g->stream);
+  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+  std::vector<int64_t> all((size_t)W * P);
+  PR_HIP(hipMemcpyAsync(all.data(), d.as<int64_t>() + W, sizeof(int64_t) * W * P, hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  for (int q = 0; q < P; ++q) {
+    const int64_t *o = all.data() + (size_t)q * W;
+    if (o[0] != g->V || o[1] != g->S_pad) return fail(PR_ERR_INVALID, "ranks hold parts of different graphs");
+    if (o[2] != mine[2]) return fail(PR_ERR_INVALID, "ranks disagree on PR_EXCHANGE");
+    if (q != g->part && !g->x_allgather && o[3 + g->part] != g->x_roff[q + 1] - g->x_roff[q])
+      return fail(PR_ERR_STATE, "exchange lists disagree between ranks");
+  }
+  return PR_OK;
+}
+
+// One process per GPU (RCCL).
+int exchange(pr_graph *g, int buf) {
+  if (g->nparts <= 1) return PR_OK;
+  if (!g->comm) return fail(PR_ERR_STATE, "graph part has no communicator (pr_graph_attach_comm)");
+  double *base = g->cbuf[buf].as<double>();
+  if (g->x_allgather) {  // whole slices, in place
+    ncclResult_t rc = ncclAllGather(base + (int64_t)g->part * g->S_pad, base, (size_t)g->S_pad, ncclDouble, g->comm,
+                                    g->stream);
+    if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+    return PR_OK;
+  }
+  PR_TRY(exchange_pack(g, buf));
+  ncclResult_t rc = ncclGroupStart();
+  for (int q = 0; q < g->nparts && rc == ncclSuccess; ++q) {
+    if (q == g->part) continue;
+    rc = ncclSend(send_runs(g, buf) + g->x_soff[q], (size_t)(g->x_soff[q + 1] - g->x_soff[q]), ncclDouble, q,
+                  g->comm, g->stream);
+    if (rc == ncclSuccess)
+      rc = ncclRecv(g->x_rbuf.as<double>() + g->x_roff[q], (size_t)(g->x_roff[q + 1] - g->x_roff[q]), ncclDouble, q,
+                    g->comm, g->stream);
+  }
+  const ncclResult_t rc2 = ncclGroupEnd();
+  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(rc));
+  if (rc2 != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(rc2));
+  return exchange_unpack(g, buf);
+}
+
+// One process, several parts: the same packed runs moved by device copies (peer copies over xGMI
+// when the parts live on different GPUs), pulled by the receiver on its stream after p's pack.
+// p's next pack goes to its other send buffer; the one after that is ordered behind q's copies
+// by p's wait on q's event in the next exchange.  q's receive buffer is only touched on q's
+// stream.
+int group_exchange(pr_graph *const *parts, int n, int buf) {
+  if (n <= 1) return PR_OK;
+  const bool whole = parts[0]->x_allgather;
+  for (int p = 0; p < n; ++p) {
+    PR_HIP(hipSetDevice(parts[p]->device));
+    if (!whole) PR_TRY(exchange_pack(parts[p], buf));
+    PR_HIP(hipEventRecord(parts[p]->xev, parts[p]->stream));
+  }
+  for (int q = 0; q < n; ++q) {
+    pr_graph *g = parts[q];
+    PR_HIP(hipSetDevice(g->device));
+    for (int p = 0; p < n; ++p) {
+      if (p == q) continue;
+      PR_HIP(hipStreamWaitEvent(g->stream, parts[p]->xev, 0));
+      if (whole) {
+        const int64_t off = (int64_t)p * g->S_pad;
+        PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + off, parts[p]->cbuf[buf].as<double>() + off,
+                              sizeof(double) * g->S_pad, hipMemcpyDeviceToDevice, g->stream));
+      } else {
+        const pr_graph *src = parts[p];
+        const int64_t cnt = g->x_roff[p + 1] - g->x_roff[p];
+        if (cnt != src->x_soff[q + 1] - src->x_soff[q]) return fail(PR_ERR_STATE, "exchange lists disagree");
+        PR_HIP(hipMemcpyAsync(g->x_rbuf.as<double>() + g->x_roff[p], send_runs(src, buf) + src->x_soff[q],
+                              sizeof(double) * cnt, hipMemcpyDeviceToDevice, g->stream));
+      }
+    }
+    if (!whole) PR_TRY(exchange_unpack(g, buf));
+  }
+  return PR_OK;
+}
+
+}  // namespace pr

@@ -92,6 +92,13 @@ struct pr_graph {
   std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;  // indices into ev_pool
   size_t ev_next = 0;
 
+  // exchange (P > 1, pr_exchange.hip): absolute gather-space positions this part sends to /
+  // receives from every peer (runs in peer order, each closed by the peer's two slots), the
+  // runs' offsets, and the packed buffers
+  pr::DevBuf x_send, x_recv, x_sbuf, x_rbuf;
+  std::vector<int64_t> x_soff, x_roff;
+  bool x_allgather = false;  // PR_EXCHANGE=allgather: whole slices instead
+
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_size = 1;
@@ -110,6 +117,9 @@ int launch_hot(pr_graph *g, int in_buf);  // the heavy-row pass (k_spmv_hot) on 
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
 int group_exchange(pr_graph *const *parts, int n, int buf);
+int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
+                   const int32_t *gpos);
 int exchange(pr_graph *g, int buf);
+int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
 }  // namespace pr

@@ -272,26 +272,6 @@ int iter_step(pr_graph *g, int32_t iterations) {
   return PR_OK;
 }
 
-// Single-process group: every part's slice (+ slots) is copied into every other part's gather
-// buffer after that part's finalize -- an all-gather by device copies (peer copies over xGMI
-// when the parts live on different GPUs).  Stream order: part p's copies wait on part q's event.
-int group_exchange(pr_graph *const *parts, int n, int buf) {
-  if (n <= 1) return PR_OK;
-  for (int q = 0; q < n; ++q) PR_HIP(hipEventRecord(parts[q]->xev, parts[q]->stream));
-  for (int p = 0; p < n; ++p) {
-    pr_graph *g = parts[p];
-    PR_HIP(hipSetDevice(g->device));
-    for (int q = 0; q < n; ++q) {
-      if (q == p) continue;
-      PR_HIP(hipStreamWaitEvent(g->stream, parts[q]->xev, 0));
-      const int64_t off = (int64_t)q * g->S_pad;
-      PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + off, parts[q]->cbuf[buf].as<double>() + off,
-                            sizeof(double) * g->S_pad, hipMemcpyDeviceToDevice, g->stream));
-    }
-  }
-  return PR_OK;
-}
-
 int read_slots(pr_graph *g, int buf, double *dc, double *l1) {
   std::vector<double> h(2 * (size_t)g->nparts);
   for (int p = 0; p < g->nparts; ++p)

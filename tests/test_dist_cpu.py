@@ -6,8 +6,11 @@ What is exercised is the distributed *protocol* the library implements with RCCL
   * vertex order by (out-degree desc, ID asc); sorted index i -> part i % P, local row i / P;
   * gather space of P slices x S_pad doubles: contributions, then the two slots
     {dangling partial, L1 partial} at S_pad-2 / S_pad-1;
-  * one all-gather of the slices per iteration, every rank summing the P dangling partials in
-    part order (so dc is identical on every rank with no extra collective).
+  * one exchange per iteration, every rank summing the P dangling partials in part order (so dc
+    is identical on every rank with no extra collective).  Two exchanges (pr_exchange.hip):
+    "sparse" - rank p sends rank q only the positions of its slice that q's in-links read,
+    ascending, then its two slots (grouped send/recv); positions q never reads stay stale (NaN
+    here, so reading one fails the test) - and "allgather" - whole slices (PR_EXCHANGE=allgather).
 """
 import os
 
@@ -15,9 +18,6 @@ import numpy as np
 import pytest
 
 import sparky_rdd
-
-WORLD = 2
-
 
 def layout(csr, P):
     V = csr.n_vertices
@@ -30,14 +30,32 @@ def layout(csr, P):
     return order, rank_of, S_pad, gpos
 
 
-def part_iteration(rank, P, csr, order, rank_of, S_pad, gpos, iters, all_gather):
+def exchange_lists(rank, P, csr, rank_of, S_pad, gpos):
+    """Absolute gather positions rank sends to / receives from every peer (pr_exchange.hip
+    build_list): sources of cross-part in-links, deduplicated, ascending, then the two slots."""
+    V = csr.n_vertices
+    owner = rank_of % P
+    rows = np.repeat(np.arange(V), np.diff(csr.row_ptr))  # in-link rows (dst)
+    cols = csr.col_idx.astype(np.int64)  # sources
+    send, recv = {}, {}
+    for q in range(P):
+        if q == rank:
+            continue
+        s_src = np.unique(gpos[cols[(owner[cols] == rank) & (owner[rows] == q)]])
+        r_src = np.unique(gpos[cols[(owner[cols] == q) & (owner[rows] == rank)]])
+        send[q] = np.concatenate([s_src, rank * S_pad + np.array([S_pad - 2, S_pad - 1])])
+        recv[q] = np.concatenate([r_src, q * S_pad + np.array([S_pad - 2, S_pad - 1])])
+    return send, recv
+
+
+def part_iteration(rank, P, csr, order, rank_of, S_pad, gpos, iters, exchange):
     V = csr.n_vertices
     rows = order[rank::P]  # original IDs of this part's rows, local order
     n_local = rows.size
     deg = csr.out_deg[rows]
     sink = (csr.vflags[rows] & 2) != 0
     r = np.ones(n_local)
-    cbuf = np.zeros(P * S_pad)
+    cbuf = np.full(P * S_pad, np.nan)
     own = rank * S_pad
 
     def publish(rr, l1):
@@ -46,7 +64,8 @@ def part_iteration(rank, P, csr, order, rank_of, S_pad, gpos, iters, all_gather)
         sl[:n_local][nz] = rr[nz] / deg[nz]
         sl[S_pad - 2] = rr[sink].sum()
         sl[S_pad - 1] = l1
-        return all_gather(sl)
+        cbuf[own:own + S_pad] = sl
+        return exchange(cbuf)
 
     cbuf = publish(r, 0.0)
     hist = []
@@ -67,7 +86,7 @@ def part_iteration(rank, P, csr, order, rank_of, S_pad, gpos, iters, all_gather)
     return hist
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     import torch
     import torch.distributed as dist
 
@@ -83,12 +102,26 @@ def _worker(rank, world, port, q):
         csr = oracle_c.build_csr(len(names), np.array(src, np.int32), np.array(dst, np.int32))
         order, rank_of, S_pad, gpos = layout(csr, world)
 
-        def all_gather(sl):
+        own = rank * S_pad
+        send, recv = exchange_lists(rank, world, csr, rank_of, S_pad, gpos)
+
+        def all_gather(cbuf):
             parts = [torch.zeros(S_pad, dtype=torch.float64) for _ in range(world)]
-            dist.all_gather(parts, torch.from_numpy(sl))
+            dist.all_gather(parts, torch.from_numpy(cbuf[own:own + S_pad].copy()))
             return torch.cat(parts).numpy()
 
-        hist = part_iteration(rank, world, csr, order, rank_of, S_pad, gpos, 6, all_gather)
+        def sparse(cbuf):
+            bufs = {p: torch.empty(len(recv[p]), dtype=torch.float64) for p in recv}
+            ops = [dist.P2POp(dist.isend, torch.from_numpy(cbuf[send[p]]), p) for p in send]
+            ops += [dist.P2POp(dist.irecv, bufs[p], p) for p in recv]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            for p in recv:
+                cbuf[recv[p]] = bufs[p].numpy()
+            return cbuf
+
+        ex = sparse if mode == "sparse" else all_gather
+        hist = part_iteration(rank, world, csr, order, rank_of, S_pad, gpos, 6, ex)
         q.put((rank, [(h[0].tolist(), h[1].tolist(), h[2]) for h in hist]))
     finally:
         dist.destroy_process_group()
@@ -105,7 +138,8 @@ def make_lines():
     return lines
 
 
-def test_two_rank_gloo_partitioned_iteration(oracle_c):
+@pytest.mark.parametrize("world,mode", [(2, "allgather"), (2, "sparse"), (3, "sparse")])
+def test_gloo_partitioned_iteration(oracle_c, world, mode):
     import socket
 
     import torch.multiprocessing as mp
@@ -115,10 +149,10 @@ def test_two_rank_gloo_partitioned_iteration(oracle_c):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(WORLD))
+    res = dict(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -131,12 +165,12 @@ def test_two_rank_gloo_partitioned_iteration(oracle_c):
     for it in range(6):
         merged = np.full(csr.n_vertices, np.nan)
         dcs = []
-        for r in range(WORLD):
+        for r in range(world):
             rows, vals, dc = res[r][it]
             merged[rows] = vals
             dcs.append(dc)
         assert not np.isnan(merged).any()  # the parts cover every vertex exactly once
-        assert dcs[0] == dcs[1]  # every rank derives the same dc from the gathered slots
+        assert len(set(dcs)) == 1  # every rank derives the same dc from the exchanged slots
         assert np.max(np.abs(merged - ref["history"][it]) / ref["history"][it]) < 1e-12
         assert abs(dcs[0] - ref["dc"][it]) <= 1e-12 * max(ref["dc"][it], 1)
 
@@ -152,3 +186,19 @@ def test_layout_balances_parts(oracle_c):
         assert max(sizes) - min(sizes) <= 1
         assert len(set(gpos.tolist())) == csr.n_vertices  # gather positions are distinct
         assert np.all(gpos % S_pad < S_pad - 2)  # never on a slot
+
+
+def test_sparse_exchange_lists_pair_up(oracle_c):
+    """What rank p sends rank q is, position for position, what q expects from p."""
+    lines = make_lines()
+    pairs = sparky_rdd.pairs_from_edge_lines(lines)
+    names, src, dst = sparky_rdd.intern_first_appearance(pairs)
+    csr = oracle_c.build_csr(len(names), np.array(src, np.int32), np.array(dst, np.int32))
+    for P in (2, 3, 4):
+        order, rank_of, S_pad, gpos = layout(csr, P)
+        lists = [exchange_lists(p, P, csr, rank_of, S_pad, gpos) for p in range(P)]
+        for p in range(P):
+            for q in range(P):
+                if p != q:
+                    assert np.array_equal(lists[p][0][q], lists[q][1][p])
+                    assert np.all(lists[p][0][q] // S_pad == p)

@@ -363,11 +363,17 @@ def test_lj_shaped_full_size(hip, oracle_c):
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
 
 
+@pytest.mark.parametrize("xmode", ["sparse", "allgather"])
 @pytest.mark.parametrize("layout", ["fused", "split"])
-@pytest.mark.parametrize("P", [2, 3, 4])
-def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout):
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode, monkeypatch):
     """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
-    exchange is the group's device-copy all-gather (RCCL carries it across processes)."""
+    exchange moves the packed per-peer runs (or whole slices, PR_EXCHANGE=allgather) by device
+    copies (RCCL send/recv carries the same runs across processes)."""
+    if xmode == "allgather":
+        monkeypatch.setenv("PR_EXCHANGE", "allgather")
+    else:
+        monkeypatch.delenv("PR_EXCHANGE", raising=False)
     rng = np.random.default_rng(30 + P)
     V = 40000
     src, dst = random_edges(rng, V, 500000, hub_frac=0.05)
@@ -379,6 +385,20 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout):
         infos = [p.info() for p in parts]
         assert sum(i["local_rows"] for i in infos) == V
         assert sum(i["local_edges"] for i in infos) == csr.n_edges
+        # sparse exchange: what the parts send is what they receive, and each part receives at
+        # most the sources of its in-links from other parts (+ 2 slots per peer)
+        if xmode == "sparse":
+            assert sum(i["xchg_send"] for i in infos) == sum(i["xchg_recv"] for i in infos)
+        rank_of = np.empty(V, np.int64)
+        rank_of[np.lexsort((np.arange(V), -csr.out_deg))] = np.arange(V)
+        owner = rank_of % P
+        rows = np.repeat(np.arange(V), np.diff(csr.row_ptr))
+        for q, i in enumerate(infos):
+            need = np.unique(csr.col_idx[(owner[rows] == q) & (owner[csr.col_idx] != q)])
+            if xmode == "sparse":
+                assert i["xchg_recv"] == len(need) + 2 * (P - 1)
+            else:
+                assert i["xchg_recv"] == (P - 1) * (i["xchg_send"])
         grp = hip.PartGroup(parts)
         r = grp.run(10)
         assert not np.isnan(r).any()

@@ -1,0 +1,87 @@
+"""P parts of one graph in one process on one GPU (pr_group_*): exchange volume of the sparse
+exchange vs whole slices, per-iteration time, and the ranks against the single-part run.
+
+    python tools/group_bench.py --scale 24 --parts 2,4,8 [--iters 10]
+
+Each part's exchange runs as device copies here; the numbers that matter for the RCCL path are
+the per-rank volumes (xchg_send / xchg_recv, doubles per iteration) and the pack/unpack cost.
+Set PR_EXCHANGE=allgather for the whole-slice A/B (read at build time).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "pagerank-using-apache-spark_amd"))
+
+
+def main():
+    import torch
+
+    import sparky_hip
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--edge-factor", type=int, default=16)
+    ap.add_argument("--parts", default="2,4,8")
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    E = a.edge_factor << a.scale
+    s = torch.empty(E, dtype=torch.int32, device="cuda")
+    d = torch.empty(E, dtype=torch.int32, device="cuda")
+    sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=1)
+    V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    torch.cuda.synchronize()
+
+    def run(P):
+        parts = [sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, part=p,
+                                          n_parts=P, keep_canonical=False) for p in range(P)]
+        try:
+            infos = [p.info() for p in parts]
+            if P == 1:
+                g = parts[0]
+                g.reset()
+                g.step(1)
+                g.sync()
+                t0 = time.perf_counter()
+                g.step(a.iters)
+                g.sync()
+                dt = time.perf_counter() - t0
+                r = np.empty(V)
+                g.ranks(r)
+            else:
+                grp = sparky_hip.PartGroup(parts)
+                grp.reset()
+                grp.step(1)
+                grp.sync()
+                t0 = time.perf_counter()
+                grp.step(a.iters)
+                grp.sync()
+                dt = time.perf_counter() - t0
+                # the ranks after 1 + iters iterations
+                r = grp.ranks()
+            return r, dt / a.iters * 1e3, infos
+        finally:
+            for p in parts:
+                p.close()
+
+    r1, ms1, _ = run(1)
+    print(json.dumps({"scale": a.scale, "V": V, "parts": 1, "ms_per_iter": round(ms1, 3)}), flush=True)
+    for P in [int(x) for x in a.parts.split(",")]:
+        r, ms, infos = run(P)
+        rel = float(np.max(np.abs(r - r1) / np.abs(r1)))
+        send = [i["xchg_send"] for i in infos]
+        recv = [i["xchg_recv"] for i in infos]
+        whole = [(P - 1) * (i["local_rows"] + 2) for i in infos]
+        print(json.dumps({"scale": a.scale, "parts": P, "mode": os.environ.get("PR_EXCHANGE", "sparse"),
+                          "ms_per_iter_all_parts_one_gpu": round(ms, 3), "max_rel_vs_1part": rel,
+                          "xchg_recv_doubles": recv, "xchg_send_doubles": send,
+                          "recv_frac_of_allgather": round(sum(recv) / max(sum(whole), 1), 4)}), flush=True)
+        assert rel <= 1e-11, rel
+
+
+if __name__ == "__main__":
+    main()
