@@ -103,7 +103,8 @@ int pr_graph_create(int32_t device, int32_t n_vertices, int64_t n_edges, const i
                     const int32_t *dst, uint32_t flags, pr_graph **out);
 
 /* The same, keeping only the rows of `part` out of `n_parts` (1D row partition for one
- * process per GPU).  Every part must be created from the same edge list. */
+ * process per GPU; 1 <= n_parts <= 64).  Every part must be created from the same edge list;
+ * the part also derives which contributions it exchanges with every peer. */
 int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices,
                          int64_t n_edges, const int32_t *src, const int32_t *dst, uint32_t flags,
                          pr_graph **out);

@@ -45,7 +45,7 @@ size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
   b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
-  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_recv.bytes + x_sbuf.bytes + x_rbuf.bytes;
+  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
   return b;
 }
 
@@ -80,6 +80,7 @@ int create_common(int32_t device, int32_t part, int32_t n_parts, int32_t n_verti
   if (!out) return fail(PR_ERR_INVALID, "out is NULL");
   *out = nullptr;
   if (n_parts < 1 || part < 0 || part >= n_parts) return fail(PR_ERR_INVALID, "bad part / n_parts");
+  if (n_parts > pr::kMaxParts) return fail(PR_ERR_INVALID, "n_parts above 64 is not supported");
   if (n_vertices < 0 || n_edges < 0) return fail(PR_ERR_INVALID, "negative size");
   if (n_edges > 0 && (!src || !dst)) return fail(PR_ERR_INVALID, "src/dst is NULL");
   if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT))
@@ -333,6 +334,7 @@ static int check_group(pr_graph *const *parts, int32_t n) {
     if (g->nparts != n || g->part != p) return fail(PR_ERR_INVALID, "parts[p] must be part p of n_parts");
     if (g->V != parts[0]->V || g->S_pad != parts[0]->S_pad) return fail(PR_ERR_INVALID, "parts of different graphs");
     if (g->comm) return fail(PR_ERR_STATE, "a part with an RCCL communicator cannot join a group");
+    if (g->x_allgather != parts[0]->x_allgather) return fail(PR_ERR_INVALID, "parts built with different PR_EXCHANGE");
   }
   return PR_OK;
 }

@@ -355,10 +355,39 @@ static void plan_class_units(const std::vector<int64_t> &rp, int64_t lo, int x, 
 
 // Entry code (pr_internal.h); a segment end is marked in bit 0 until k_unit_meta moves it into
 // the lane metadata (codes are byte offsets / addresses, multiples of 8).
-__device__ __forceinline__ uint32_t hot_code(int32_t pos, int x, const HotGeom &hg, bool end) {
-  const int64_t p = pos / hg.S_pad, w = pos - p * hg.S_pad, y = w / hg.Q_pad, q = w - y * hg.Q_pad;
-  const uint32_t c = (y == x && q < hg.Kp) ? (uint32_t)(8 * (1 + p * hg.Kp + q)) : (kEntGlobal | ((uint32_t)pos * 8u));
+// hpos[x * P*Kp + p*Kp + q] = gather position of row x*Q_pad + q of part p (0 when q >= q_load or
+// the part never reads it: the slot is then never addressed); hotidx[pos] = its LDS slot.
+__global__ void k_hot_tables(HotGeom hg, const int32_t *__restrict__ cmap, int32_t *__restrict__ hpos,
+                             int32_t *__restrict__ hotidx) {
+  const int64_t nh = (int64_t)hg.P * hg.Kp;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < (int64_t)hg.C * nh;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = t / nh, i = t - x * nh, p = i / hg.Kp, q = i - p * hg.Kp;
+    int32_t pos = -1;
+    if (q < hg.q_load) {
+      const int64_t a = p * hg.S_pad + x * hg.Q_pad + q;
+      pos = cmap ? cmap[a] : (int32_t)a;
+    }
+    hpos[t] = pos < 0 ? 0 : pos;
+    if (pos >= 0) hotidx[pos] = (int32_t)(1 + i);
+  }
+}
+
+// Entry code of a gather position: its LDS byte address when hot (pr_internal.h kEntGlobal).
+__device__ __forceinline__ uint32_t hot_code(int32_t pos, const int32_t *__restrict__ hotidx, bool end) {
+  const int32_t h = hotidx[pos];
+  const uint32_t c = h ? (uint32_t)(8 * h) : (kEntGlobal | ((uint32_t)pos * 8u));
   return end ? (c | 1u) : c;
+}
+
+// Columns -> compacted gather positions; counts sources the exchange lists miss (a bug).
+__global__ void k_map_cols(int64_t n, const int32_t *__restrict__ cmap, int32_t *__restrict__ col,
+                           unsigned long long *__restrict__ bad) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = cmap[col[i]];
+    if (c < 0) atomicAdd(bad, 1ull);
+    col[i] = c < 0 ? 0 : c;
+  }
 }
 
 // Marks the last in-link of every non-empty row of a class CSR (bit 31 of the column entry;
@@ -386,13 +415,11 @@ __global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all
 __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *__restrict__ units,
                                                   const int64_t *__restrict__ src_off,
                                                   const int32_t *__restrict__ n_real,
-                                                  const int32_t *__restrict__ col, HotGeom hg,
-                                                  const int64_t *__restrict__ ucum,
+                                                  const int32_t *__restrict__ col,
+                                                  const int32_t *__restrict__ hotidx,
                                                   uint32_t *__restrict__ colh) {
   for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
     const Unit u = units[b];
-    int x = 0;
-    while (x + 1 < hg.C && ucum[x + 1] <= b) ++x;
     uint32_t *dst = colh + (int64_t)u.p8 * 8;
     const int64_t s0 = src_off[b];
     const int n = n_real[b];
@@ -400,7 +427,7 @@ __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *_
       uint32_t c = 0;
       if (i < n) {
         const int32_t v = col[s0 + i];
-        c = hot_code(v & 0x7FFFFFFF, x, hg, u.meta >= 0 && v < 0);
+        c = hot_code(v & 0x7FFFFFFF, hotidx, u.meta >= 0 && v < 0);
       }
       dst[i] = c;
     }
@@ -587,7 +614,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   g->geo = geo;
 
   // ---- exchange lists (P > 1): which of this part's contributions every peer reads ----
-  PR_TRY(build_exchange(g, ukeys, m, b, maskb, rank_of.as<int32_t>(), gpos.as<int32_t>()));
+  DevBuf cmap;  // global -> compacted gather position (P > 1, sparse exchange)
+  PR_TRY(build_exchange(g, ukeys, m, b, maskb, rank_of.as<int32_t>(), gpos.as<int32_t>(), &cmap));
 
   // ---- the part's in-link CSRs: one per column class (one in the fused layout) ----
   const int64_t R = g->n_rows;
@@ -605,6 +633,17 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   if (lm > 0)
     hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
                        keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
+  if (cmap.p && lm > 0) {  // columns -> the compacted gather space (order within rows kept)
+    DevBuf bad;
+    PR_TRY(bad.alloc(sizeof(unsigned long long)));
+    PR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_map_cols, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s, lm, cmap.as<int32_t>(),
+                       g->col.as<int32_t>(), bad.as<unsigned long long>());
+    unsigned long long hb = 0;
+    PR_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(hb), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
+    if (hb) return fail(PR_ERR_STATE, "exchange lists miss a source of this part's in-links");
+  }
   DevBuf cls_start;
   PR_TRY(cls_start.alloc(sizeof(int64_t) * (C + 1)));
   hipLaunchKernelGGL(k_class_bounds, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s,
@@ -702,6 +741,16 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
     g->hot = hg;
+    // hot-set gather positions per class, and the LDS slot of every hot gather position
+    DevBuf hotidx;
+    const int64_t nh = (int64_t)P * hg.Kp;
+    PR_TRY(g->hpos.alloc(sizeof(int32_t) * (size_t)(C * nh > 0 ? C * nh : 1)));
+    PR_TRY(hotidx.alloc(sizeof(int32_t) * (size_t)g->gsize));
+    PR_HIP(hipMemsetAsync(hotidx.p, 0, sizeof(int32_t) * (size_t)g->gsize, s));
+    if (C * nh > 0)
+      hipLaunchKernelGGL(k_hot_tables, dim3(grid_for(C * nh, T, 65536)), dim3(T), 0, s, hg,
+                         cmap.p ? cmap.as<int32_t>() : nullptr, g->hpos.as<int32_t>(), hotidx.as<int32_t>());
+    PR_HIP(hipGetLastError());
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
     g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
@@ -730,8 +779,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
       PR_HIP(hipMemcpyAsync(dsrc_off.p, wp.src_off.data(), sizeof(int64_t) * nu, hipMemcpyHostToDevice, s));
       PR_HIP(hipMemcpyAsync(dn.p, wp.n_real.data(), sizeof(int32_t) * nu, hipMemcpyHostToDevice, s));
       hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(256), 0, s, (int64_t)nu,
-                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dn.as<int32_t>(), g->col.as<int32_t>(), hg,
-                         g->hucum.as<int64_t>(), g->colh.as<uint32_t>());
+                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dn.as<int32_t>(), g->col.as<int32_t>(),
+                         hotidx.as<int32_t>(), g->colh.as<uint32_t>());
       hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(kWave), 0, s, (int64_t)nu,
                          g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
       PR_HIP(hipGetLastError());
@@ -766,8 +815,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   // ---- iteration state ----
   PR_TRY(g->r.alloc(sizeof(double) * ((size_t)g->n_rows + 1)));
   for (int k = 0; k < 2; ++k) {
-    PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)P * g->S_pad));
-    PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)P * g->S_pad, s));
+    PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)g->gsize));
+    PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)g->gsize, s));
   }
   g->fin_blocks = 512;
   PR_TRY(g->fin_part.alloc(sizeof(double) * 2 * g->fin_blocks));

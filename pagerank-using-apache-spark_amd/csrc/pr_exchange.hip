@@ -1,17 +1,18 @@
 // The exchange of the row-partitioned iteration: after its epilogue every part
-// has fresh contributions c' = r'/d for its own rows (its slice of the gather space) and the two
-// slots {dangling partial, L1 partial}.  Part q only ever reads the contributions of the sources
-// of its own in-links, so part p sends q exactly those positions of its slice (plus the two
-// slots), packed densely; q scatters them to their native positions in its copy of the gather
-// space.  Codes, hot sets and kernels are unchanged: positions q never reads stay stale.
+// has fresh contributions c' = r'/d for its own rows (its slice) and the two slots {dangling
+// partial, L1 partial}.  Part q only ever reads the contributions of the sources of its own
+// in-links, so part p sends q exactly those positions of its slice (plus the two slots), packed
+// densely, and q receives them straight into its gather space: q's gather space is its own slice
+// followed by the runs it receives, peer by peer (the compacted layout; pr_graph.h).  q's
+// column codes and hot-set table point into that space, so nothing is unpacked.
 //
 // Both ends derive the p -> q position list from the same edge list with the same rules, so they
-// agree on every count without communicating.  At R-MAT s26 with 8 parts this moves 47 % of the
-// sources an all-gather of whole slices would (and none of the sinks).
+// agree on every count without communicating (verify_exchange checks it once at attach time).
+// At R-MAT s26 with 8 parts each rank receives 39 % of what an all-gather of whole slices moves.
 //
 // Transport: RCCL grouped ncclSend / ncclRecv (one process per GPU), or device-to-device copies
-// (pr_group_*: one process, several parts).  PR_EXCHANGE=allgather restores the whole-slice
-// all-gather (A/B, diagnostics).
+// (pr_group_*: one process, several parts).  PR_EXCHANGE=allgather restores whole slices in an
+// uncompacted gather space of P slices (A/B, diagnostics).
 #include <cstdlib>
 #include <cstring>
 
@@ -61,24 +62,25 @@ struct XIdent {
   __device__ uint64_t operator()(int64_t i) const { return k[i]; }
 };
 
-// Sorted unique (peer, pos) keys -> absolute positions grouped by peer (peer order), each peer's
-// run followed by its two slot positions: out[k + 2 * peer_ordinal] for key k.
+// Sorted unique (peer, pos) keys -> positions grouped by peer (peer order), each peer's run
+// followed by its two slot positions: out[k + 2 * peer_ordinal] for key k.  Send lists hold
+// positions in this part's slice, receive lists global positions (peer * S_pad + pos).
 __global__ void k_xlist(int64_t n, const uint64_t *__restrict__ keys, const int64_t *__restrict__ first,
                         int P, int self, int64_t S_pad, bool send, uint32_t *__restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int q = (int)(keys[i] >> 32);
     const int ord = q - (q > self ? 1 : 0);
-    const int64_t owner = send ? self : q;
-    out[i + 2 * ord] = (uint32_t)(owner * S_pad + (int64_t)(keys[i] & 0xFFFFFFFFull));
+    const int64_t base = send ? 0 : (int64_t)q * S_pad;  // send: own slice; receive: global position
+    out[i + 2 * ord] = (uint32_t)(base + (int64_t)(keys[i] & 0xFFFFFFFFull));
   }
   if (blockIdx.x == 0 && threadIdx.x < P) {  // the slots close every peer's run
     const int q = threadIdx.x;
     if (q != self) {
       const int ord = q - (q > self ? 1 : 0);
-      const int64_t owner = send ? self : q;
+      const int64_t base = send ? 0 : (int64_t)q * S_pad;
       const int64_t end = first[q + 1] + 2 * ord;  // run end of peer q
-      out[end] = (uint32_t)(owner * S_pad + S_pad - 2);
-      out[end + 1] = (uint32_t)(owner * S_pad + S_pad - 1);
+      out[end] = (uint32_t)(base + S_pad - 2);
+      out[end + 1] = (uint32_t)(base + S_pad - 1);
     }
   }
 }
@@ -109,22 +111,14 @@ __global__ __launch_bounds__(256) void k_pack(int64_t n, const uint32_t *__restr
   }
 }
 
-__global__ __launch_bounds__(256) void k_unpack(int64_t n, const uint32_t *__restrict__ pos,
-                                                const double *__restrict__ in, double *__restrict__ cbuf) {
-  const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 p = reinterpret_cast<const uint4 *>(pos)[i];
-    const double2 ab = reinterpret_cast<const double2 *>(in)[2 * i];
-    const double2 cd = reinterpret_cast<const double2 *>(in)[2 * i + 1];
-    cbuf[p.x] = ab.x;
-    cbuf[p.y] = ab.y;
-    cbuf[p.z] = cd.x;
-    cbuf[p.w] = cd.y;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-    const int64_t i = (n4 << 2) + threadIdx.x;
-    cbuf[pos[i]] = in[i];
-  }
+// Compacted gather space: global position -> this part's position (-1: never read here).
+__global__ void k_cmap_own(int64_t S_pad, int part, int32_t *__restrict__ cmap) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < S_pad; j += (int64_t)gridDim.x * blockDim.x)
+    cmap[(int64_t)part * S_pad + j] = (int32_t)j;
+}
+__global__ void k_cmap_recv(int64_t n, const uint32_t *__restrict__ recv, int64_t S_pad, int32_t *__restrict__ cmap) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    cmap[recv[k]] = (int32_t)(S_pad + k);
 }
 
 bool allgather_requested() {
@@ -178,16 +172,38 @@ double *send_runs(const pr_graph *g, int buf) {
 }
 
 int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
-                   const int32_t *gpos) {
-  g->x_allgather = allgather_requested();
-  if (g->nparts <= 1 || g->x_allgather) return PR_OK;
+                   const int32_t *gpos, DevBuf *cmap) {
+  const int P = g->nparts, self = g->part;
+  g->x_allgather = P > 1 && allgather_requested();
+  g->slots.n = P;
+  if (P <= 1 || g->x_allgather) {  // P slices side by side
+    g->gsize = (int64_t)P * g->S_pad;
+    g->own_off = (int64_t)self * g->S_pad;
+    for (int q = 0; q < P; ++q) g->slots.pos[q] = (int32_t)((int64_t)q * g->S_pad + g->S_pad - 2);
+    return PR_OK;
+  }
+  DevBuf recv;
   PR_TRY(build_list(g, ukeys, m, b, mask, rank_of, gpos, true, &g->x_send, &g->x_soff));
-  PR_TRY(build_list(g, ukeys, m, b, mask, rank_of, gpos, false, &g->x_recv, &g->x_roff));
-  const int P = g->nparts;
+  PR_TRY(build_list(g, ukeys, m, b, mask, rank_of, gpos, false, &recv, &g->x_roff));
+  const int64_t R = g->x_roff[P];
+  g->gsize = g->S_pad + R;
+  g->own_off = 0;
+  for (int q = 0; q < P; ++q)
+    g->slots.pos[q] = (int32_t)(q == self ? g->S_pad - 2 : g->S_pad + g->x_roff[q + 1] - 2);
+  hipStream_t s = g->stream;
+  const int64_t G = (int64_t)P * g->S_pad;
+  PR_TRY(cmap->alloc(sizeof(int32_t) * (size_t)G));
+  PR_HIP(hipMemsetAsync(cmap->p, 0xFF, sizeof(int32_t) * (size_t)G, s));
+  hipLaunchKernelGGL(k_cmap_own, dim3(grid_for(g->S_pad, 256, 65536)), dim3(256), 0, s, g->S_pad, self,
+                     cmap->as<int32_t>());
+  if (R > 0)
+    hipLaunchKernelGGL(k_cmap_recv, dim3(grid_for(R, 256, 65536)), dim3(256), 0, s, R, recv.as<uint32_t>(), g->S_pad,
+                       cmap->as<int32_t>());
+  PR_HIP(hipGetLastError());
   // two send buffers, one per gather-space buffer: in the group path a peer's copy out of the
   // runs of iteration k may still be pending when this part packs iteration k + 1
   PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
-  PR_TRY(g->x_rbuf.alloc(sizeof(double) * (size_t)(g->x_roff[P] > 0 ? g->x_roff[P] : 1)));
+  PR_HIP(hipStreamSynchronize(s));
   return PR_OK;
 }
 
@@ -196,15 +212,6 @@ int exchange_pack(pr_graph *g, int buf) {
   if (n > 0)
     hipLaunchKernelGGL(k_pack, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, g->stream, n, g->x_send.as<uint32_t>(),
                        g->cbuf[buf].as<double>(), send_runs(g, buf));
-  PR_HIP(hipGetLastError());
-  return PR_OK;
-}
-
-int exchange_unpack(pr_graph *g, int buf) {
-  const int64_t n = g->x_roff[g->nparts];
-  if (n > 0)
-    hipLaunchKernelGGL(k_unpack, dim3(grid_for((n + 3) / 4, 256, 8192)), dim3(256), 0, g->stream, n, g->x_recv.as<uint32_t>(),
-                       g->x_rbuf.as<double>(), g->cbuf[buf].as<double>());
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
@@ -258,19 +265,19 @@ int exchange(pr_graph *g, int buf) {
     rc = ncclSend(send_runs(g, buf) + g->x_soff[q], (size_t)(g->x_soff[q + 1] - g->x_soff[q]), ncclDouble, q,
                   g->comm, g->stream);
     if (rc == ncclSuccess)
-      rc = ncclRecv(g->x_rbuf.as<double>() + g->x_roff[q], (size_t)(g->x_roff[q + 1] - g->x_roff[q]), ncclDouble, q,
+      rc = ncclRecv(base + g->S_pad + g->x_roff[q], (size_t)(g->x_roff[q + 1] - g->x_roff[q]), ncclDouble, q,
                     g->comm, g->stream);
   }
   const ncclResult_t rc2 = ncclGroupEnd();
   if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(rc));
   if (rc2 != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(rc2));
-  return exchange_unpack(g, buf);
+  return PR_OK;
 }
 
 // One process, several parts: the same packed runs moved by device copies (peer copies over xGMI
 // when the parts live on different GPUs), pulled by the receiver on its stream after p's pack.
 // p's next pack goes to its other send buffer; the one after that is ordered behind q's copies
-// by p's wait on q's event in the next exchange.  q's receive buffer is only touched on q's
+// by p's wait on q's event in the next exchange.  q's gather space is only written on q's
 // stream.
 int group_exchange(pr_graph *const *parts, int n, int buf) {
   if (n <= 1) return PR_OK;
@@ -294,11 +301,10 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
         const pr_graph *src = parts[p];
         const int64_t cnt = g->x_roff[p + 1] - g->x_roff[p];
         if (cnt != src->x_soff[q + 1] - src->x_soff[q]) return fail(PR_ERR_STATE, "exchange lists disagree");
-        PR_HIP(hipMemcpyAsync(g->x_rbuf.as<double>() + g->x_roff[p], send_runs(src, buf) + src->x_soff[q],
+        PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + g->S_pad + g->x_roff[p], send_runs(src, buf) + src->x_soff[q],
                               sizeof(double) * cnt, hipMemcpyDeviceToDevice, g->stream));
       }
     }
-    if (!whole) PR_TRY(exchange_unpack(g, buf));
   }
   return PR_OK;
 }

@@ -2,29 +2,26 @@
 //
 // HBM layout of one part (DESIGN.md "Data layout"):
 //   internal vertex order   vertices sorted by (out-degree desc, original ID asc); sorted index
-//                           i is owned by part i % P as local row i / P.  Hot sources (high
-//                           out-degree = most-gathered contribution) sit together at the front.
-//   gather space            P slices of S_pad doubles; slice p = contributions c of part p's
-//                           rows, then two slots {dangling partial, L1 partial}.  col_idx holds
-//                           positions in this space, so the RCCL all-gather of the slices is
-//                           the whole exchange (one call per iteration).
-//   rowptr  int64[n_local+1]  in-link CSR of the part's rows (local row order)
-//   colp    int32[padded nnz]  gather positions, ascending within a row, grouped by work unit,
-//                             every unit 32-byte aligned (pr_spmv.h loads them as int4)
+//                           i is owned by part i % P as local rank j = i / P.  Hot sources (high
+//                           out-degree = most-gathered contributions) sit together at the front.
+//   slice                   S_pad doubles per part: the contributions c = r/d of its rows, then
+//                           two slots {dangling partial, L1 partial}.
+//   gather space (cbuf)     what this part's in-links read: P slices side by side (P = 1,
+//                           PR_EXCHANGE=allgather), or - the default for P > 1 - this part's
+//                           slice followed by the runs it receives from every peer (only the
+//                           sources of its own in-links; pr_exchange.hip).  Double-buffered.
 //   rowinfo uint32[R]         out-degree | kRowSink (in D) | kRowIndeg0 | kRowHole
 //   r       fp64[R]           ranks, updated in place
 //
-// Column classes (C = 8 once a part's contribution slice exceeds the L2s, else C = 1): local
-// rank j -> class j % C; a slice is C contiguous regions of Q_pad rows, so row L = x*Q_pad + q is
-// also the gather position inside the slice (holes pad the last region).  In-links are split by
-// the class of their source; class-x work units run at blockIdx % 8 == x, i.e. on one XCD, whose
-// 4 MiB L2 then caches only class-x contributions (8x the aggregate L2 reach for the gathers).
-// Only heavy rows (>= kHeavyMinIndeg in-links; a prefix of every region, since heavy vertices
-// sort first) are split: heavy row h has C partial slots partial[x][h] that an epilogue pass
-// adds in class order.  Light rows keep the fused single pass (pr_spmv.h k_spmv_units).
-// Heavy rows are processed as wave units whose entries address either the gather space or the
-// class's LDS hot set: the first Kp positions of every part's class-x region (pr_internal.h).
-//   cbuf    fp64[2][P*S_pad]  contributions r/d, double-buffered across iterations
+// Column classes (C = 16 by default once the whole gather space outgrows the L2s, else C = 1):
+// local rank j -> class x = j % C, row L = x*Q_pad + j/C (also its position in the slice).
+// Split layout (C > 1): every row's in-links are split by the class of their source; each
+// non-empty (row, class) pair is a segment with one slot of a class-dense partial array.  Class-x
+// wave units run on one XCD (two classes per XCD), whose L2 then caches only class-x sources, and
+// address either the gather space or the class's LDS hot set (the first Kp rows of every part's
+// class-x region; pr_internal.h HotGeom, positions from the hpos table).  k_epilogue adds a row's
+// segment sums in class order.  Fused layout (C = 1, small graphs): rowptr/colp CSR with
+// 256-thread units and the update fused into the same kernel (pr_spmv.h k_spmv_units).
 #pragma once
 
 #include <rccl/rccl.h>
@@ -63,8 +60,8 @@ struct pr_graph {
   // and lane metadata; per class x the partial sums of its segments at partial[poff[x] + slot];
   // per row the mask of classes with in-links (rmask) and per class the slot of the first
   // segment of every 64-row block (cbase[blk][x]); long segments: pieces reduced in order into
-  // partial[seg_slot[q]]
-  pr::DevBuf colh, hmeta, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0;
+  // partial[seg_slot[q]]; hpos[x * P*Kp + i]: gather position of LDS hot slot 1 + i of class x
+  pr::DevBuf colh, hmeta, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};
@@ -92,10 +89,15 @@ struct pr_graph {
   std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;  // indices into ev_pool
   size_t ev_next = 0;
 
-  // exchange (P > 1, pr_exchange.hip): absolute gather-space positions this part sends to /
-  // receives from every peer (runs in peer order, each closed by the peer's two slots), the
-  // runs' offsets, and the packed buffers
-  pr::DevBuf x_send, x_recv, x_sbuf, x_rbuf;
+  // gather space (doubles per cbuf): P slices side by side (P = 1, PR_EXCHANGE=allgather), or
+  // compacted: this part's slice, then the runs received from every peer in peer order
+  int64_t gsize = 0;
+  int64_t own_off = 0;  // this part's slice in the gather space
+  pr::SlotPos slots{};  // every part's slot pair in the gather space
+  // exchange (P > 1, pr_exchange.hip): positions of this part's slice sent to every peer (runs
+  // in peer order, each closed by the two slots), run offsets of what it sends / receives
+  // (received runs land at S_pad + x_roff[p]), and the double-buffered packed send runs
+  pr::DevBuf x_send, x_sbuf;
   std::vector<int64_t> x_soff, x_roff;
   bool x_allgather = false;  // PR_EXCHANGE=allgather: whole slices instead
 
@@ -117,8 +119,10 @@ int launch_hot(pr_graph *g, int in_buf);  // the heavy-row pass (k_spmv_hot) on 
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
 int group_exchange(pr_graph *const *parts, int n, int buf);
+// Exchange lists and the gather-space geometry (gsize, own_off, slots); *cmap receives the
+// global -> compacted position map (-1: not read by this part) when the space is compacted.
 int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
-                   const int32_t *gpos);
+                   const int32_t *gpos, DevBuf *cmap);
 int exchange(pr_graph *g, int buf);
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);

@@ -139,8 +139,17 @@ struct PartOff {
   int64_t o[kMaxClasses + 1];
 };
 
-// Where a class's hot contributions live in the gather space: for every part p, positions
-// [p*S_pad + x*Q_pad, + q_load) go to LDS slots 1 + [p*Kp, p*Kp + q_load); slot 0 holds 0.0.
+// Gather positions of every part's {dangling partial, L1 partial} slot pair (the dangling one;
+// L1 follows), in part order.  Passed by value: the kernels read them as scalars.
+constexpr int kMaxParts = 64;
+struct SlotPos {
+  int n;
+  int32_t pos[kMaxParts];
+};
+
+// A class's hot set: for every part p, rows [x*Q_pad, + q_load) of p's slice go to LDS slots
+// 1 + [p*Kp, p*Kp + q_load); slot 0 holds 0.0.  Their gather positions come from a table (the
+// part's gather space is compacted when only some remote positions are received).
 struct HotGeom {
   int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
     int64_t n_long, const int32_t *__restrict__ lr_row, const int32_t *__restrict__ lr_p0,
     const double *__restrict__ piece_part, const double2 *__restrict__ parts, int64_t n_parts,
     double *__restrict__ r, const uint32_t *__restrict__ rowinfo, const double *__restrict__ cin,
-    double *__restrict__ cout, int P, int64_t S_pad, double n_vertices, double teleport,
+    double *__restrict__ cout, SlotPos sp, double n_vertices, double teleport,
     double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
     double *__restrict__ slot_out) {
   __shared__ double red[kThreads / kWave];
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
   const int t = threadIdx.x, lane = lane_id();
   double dcp = 0.0, l1p = 0.0;
   if (n_long > 0) {
-    const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+    const double tdc = dc_from_slots(cin, sp) / n_vertices;
     const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);
     for (int64_t q = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); q < n_long; q += nw) {
       const int32_t p0 = lr_p0[q], np = lr_p0[q + 1] - p0;
@@ -137,12 +137,11 @@ hipEvent_t next_event(pr_graph *g) {
 
 int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n_parts, int in_buf,
                     int out_buf) {
-  const int64_t own = (int64_t)g->part * g->S_pad;
-  double *cout = g->cbuf[out_buf].as<double>() + own;
+  double *cout = g->cbuf[out_buf].as<double>() + g->own_off;
   hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, g->stream, n_long,
                      g->lr_row.as<int32_t>(), g->lr_p0.as<int32_t>(), g->piece_part.as<double>(),
                      parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
-                     g->cbuf[in_buf].as<double>(), cout, g->nparts, g->S_pad, (double)g->V,
+                     g->cbuf[in_buf].as<double>(), cout, g->slots, (double)g->V,
                      g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
                      cout + g->S_pad - 2);
   PR_HIP(hipGetLastError());
@@ -162,8 +161,8 @@ int launch_hot(pr_graph *g, int in) {
   hipLaunchKernelGGL((k_spmv_hot<0, 0>), dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
                      g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
-                     (uint32_t)(sizeof(double) * g->nparts * g->S_pad), g->partial.as<double>(),
-                     g->poff.as<int64_t>(), g->piece_part.as<double>());
+                     (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),
+                     g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>());
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
@@ -180,7 +179,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
     PR_HIP(hipStreamSynchronize(s));
   }
   g->cur = 0;
-  const int64_t own = (int64_t)g->part * g->S_pad;
+  const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
                      dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
@@ -199,7 +198,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
 
 int iter_compute(pr_graph *g) {
   hipStream_t s = g->stream;
-  const int64_t own = (int64_t)g->part * g->S_pad;
+  const int64_t own = g->own_off;
   const int in = g->cur, out = g->cur ^ 1;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g->timing) {
@@ -214,7 +213,7 @@ int iter_compute(pr_graph *g) {
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
                        g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
                        g->rowinfo.as<uint32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
-                       g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
+                       g->slots, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
   int64_t n_parts = g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
     if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
@@ -226,7 +225,7 @@ int iter_compute(pr_graph *g) {
                        dim3(kThreads), 0, s, g->nblk, g->part_off, g->partial.as<double>(),
                        g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(),
                        g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
-                       g->cbuf[in].as<double>(), g->nparts, g->S_pad, (double)g->V, g->teleport, g->damping,
+                       g->cbuf[in].as<double>(), g->slots, (double)g->V, g->teleport, g->damping,
                        g->unit_part.as<double2>() + g->n_units);
     n_parts += g->ep_blocks;
   }
@@ -275,8 +274,8 @@ int iter_step(pr_graph *g, int32_t iterations) {
 int read_slots(pr_graph *g, int buf, double *dc, double *l1) {
   std::vector<double> h(2 * (size_t)g->nparts);
   for (int p = 0; p < g->nparts; ++p)
-    PR_HIP(hipMemcpyAsync(&h[2 * p], g->cbuf[buf].as<double>() + (int64_t)p * g->S_pad + g->S_pad - 2,
-                          2 * sizeof(double), hipMemcpyDeviceToHost, g->stream));
+    PR_HIP(hipMemcpyAsync(&h[2 * p], g->cbuf[buf].as<double>() + g->slots.pos[p], 2 * sizeof(double),
+                          hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
   double a = 0.0, b = 0.0;
   for (int p = 0; p < g->nparts; ++p) {

@@ -25,9 +25,10 @@
 
 namespace pr {
 
-__device__ __forceinline__ double dc_from_slots(const double *cin, int P, int64_t S_pad) {
+// dc = the parts' dangling partials added in part order (identical on every part)
+__device__ __forceinline__ double dc_from_slots(const double *cin, const SlotPos &sp) {
   double dc = 0.0;
-  for (int p = 0; p < P; ++p) dc = __dadd_rn(dc, cin[(int64_t)p * S_pad + S_pad - 2]);
+  for (int p = 0; p < sp.n; ++p) dc = __dadd_rn(dc, cin[sp.pos[p]]);
   return dc;
 }
 
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
     const Unit *__restrict__ units, const int64_t *__restrict__ rowptr,
     const int32_t *__restrict__ colp, const double *__restrict__ cin, double *__restrict__ cout,
     double *__restrict__ r, const uint32_t *__restrict__ rowinfo, double *__restrict__ piece_part,
-    double2 *__restrict__ unit_part, int P, int64_t S_pad, double n_vertices, double teleport,
+    double2 *__restrict__ unit_part, SlotPos sp, int64_t S_pad, double n_vertices, double teleport,
     double damping, uint32_t gather_mask) {
   __shared__ double rowsum[kUnitRows];
   __shared__ int32_t lrp[kUnitRows + 1];
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(kThreads) void k_spmv_units(
   const int64_t e0 = rowptr[r0];
   if (t <= nr) lrp[t] = (int32_t)(rp_t - e0);
   for (int k = t + kThreads; k <= nr; k += kThreads) lrp[k] = (int32_t)(rowptr[r0 + k] - e0);
-  const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+  const double tdc = dc_from_slots(cin, sp) / n_vertices;
   __syncthreads();
 
   int carry_row = -1, first_row = -1;
@@ -401,17 +402,16 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           const double *__restrict__ cin, uint32_t cin_bytes,
                                                           double *__restrict__ partial,
                                                           const int64_t *__restrict__ poff,
-                                                          double *__restrict__ piece_part) {
+                                                          double *__restrict__ piece_part,
+                                                          const int32_t *__restrict__ hpos) {
   extern __shared__ double hot[];
   // class x runs on XCD x % 8 (round-robin dispatch: workgroup b on XCD b % 8)
   const int x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
   const int team = (int)(blockIdx.x / hg.C), nteams = (int)(gridDim.x / hg.C);
   // stage the class's hot contributions (the previous iteration's, final before this launch)
   const int nh = hg.P * hg.Kp;
-  for (int i = threadIdx.x; i < nh; i += kHotThreads) {
-    const int p = i / hg.Kp, q = i - p * hg.Kp;
-    hot[1 + i] = q < hg.q_load ? cin[(int64_t)p * hg.S_pad + (int64_t)x * hg.Q_pad + q] : 0.0;
-  }
+  const int32_t *hp = hpos + (int64_t)x * nh;
+  for (int i = threadIdx.x; i < nh; i += kHotThreads) hot[1 + i] = cin[hp[i]];
   if (threadIdx.x == 0) hot[0] = 0.0;
   __syncthreads();
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
@@ -486,12 +486,12 @@ __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po,
                                                        const int32_t *__restrict__ cbase,
                                                        const uint32_t *__restrict__ rowinfo,
                                                        double *__restrict__ r, double *__restrict__ cout,
-                                                       const double *__restrict__ cin, int P, int64_t S_pad,
+                                                       const double *__restrict__ cin, SlotPos sp,
                                                        double n_vertices, double teleport, double damping,
                                                        double2 *__restrict__ ep_part) {
   typedef int cb_t __attribute__((ext_vector_type(C)));
   __shared__ double2 red2[kThreads / kWave];
-  const double tdc = dc_from_slots(cin, P, S_pad) / n_vertices;
+  const double tdc = dc_from_slots(cin, sp) / n_vertices;
   const int lane = lane_id();
   double dcp = 0.0, l1p = 0.0;
   const int64_t nw = (int64_t)gridDim.x * (kThreads / kWave);

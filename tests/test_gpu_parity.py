@@ -363,6 +363,29 @@ def test_lj_shaped_full_size(hip, oracle_c):
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
 
 
+@pytest.mark.parametrize("layout", ["fused", "split"])
+def test_compacted_gather_space_is_bitwise_whole_slices(hip, layout, monkeypatch):
+    """The compacted gather space (own slice + received runs) keeps every row's summation order,
+    so its ranks equal the whole-slice all-gather layout's bit for bit."""
+    rng = np.random.default_rng(77)
+    V = 30000
+    src, dst = random_edges(rng, V, 300000, hub_frac=0.05)
+    out = {}
+    for xmode in ("sparse", "allgather"):
+        if xmode == "allgather":
+            monkeypatch.setenv("PR_EXCHANGE", "allgather")
+        else:
+            monkeypatch.delenv("PR_EXCHANGE", raising=False)
+        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout=layout)
+                 for p in range(3)]
+        try:
+            out[xmode] = hip.PartGroup(parts).run(8)
+        finally:
+            for p in parts:
+                p.close()
+    assert np.array_equal(out["sparse"], out["allgather"])
+
+
 @pytest.mark.parametrize("xmode", ["sparse", "allgather"])
 @pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("P", [2, 3, 4, 8])

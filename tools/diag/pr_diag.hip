@@ -62,12 +62,12 @@ int layout_for(pr_graph *g, int pt, Layout **out) {
 
 template <int PT, bool NT, bool MASK, int GM = 0, int XC = 0>
 void launch(pr_graph *g, Layout *L, uint32_t mask) {
-  const int64_t own = (int64_t)g->part * g->S_pad;
+  const int64_t own = g->own_off;
   hipLaunchKernelGGL((k_spmv_units<PT, NT, MASK, GM, XC>), dim3((unsigned)L->n_units), dim3(kThreads), 0,
                      g->stream, L->units.as<Unit>(), g->rowptr.as<int64_t>(), L->colp.as<int32_t>(),
                      g->cbuf[0].as<double>(), g->cbuf[1].as<double>() + own, g->r.as<double>(),
                      g->rowinfo.as<uint32_t>(), L->piece_part.as<double>(), L->unit_part.as<double2>(),
-                     g->nparts, g->S_pad, (double)g->V, 0.15, 0.85, mask);
+                     g->slots, g->S_pad, (double)g->V, 0.15, 0.85, mask);
 }
 
 }  // namespace
@@ -195,14 +195,16 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  const uint32_t cin_bytes = (uint32_t)(sizeof(double) * g->nparts * g->S_pad);
+  const uint32_t cin_bytes = (uint32_t)(sizeof(double) * g->gsize);
   Unit *units = g->hunits.as<Unit>();
   int64_t *ucum = g->hucum.as<int64_t>();
   HotGeom hg = g->hot;
   uint32_t *colh = g->colh.as<uint32_t>(), *hmeta = g->hmeta.as<uint32_t>();
   double *cin = g->cbuf[0].as<double>(), *partial = g->partial.as<double>(), *pp = g->piece_part.as<double>();
   int64_t *poff = g->poff.as<int64_t>();
-  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &poff, &pp};
+  int32_t *hpos = g->hpos.as<int32_t>();
+  // must match k_spmv_hot's parameter list exactly
+  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &poff, &pp, &hpos};
   hipEvent_t a, b;
   PR_HIP(hipEventCreate(&a));
   PR_HIP(hipEventCreate(&b));
