@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 METRIC = "PageRank GTEPS/iter + % HBM roofline, R-MAT scale-26 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 # bumped whenever the SpMV pass changes, so a stale rocprof traffic figure is never reported
-LAYOUT_VERSION = "masked-split-v1"
+LAYOUT_VERSION = "masked-split-c32-phased-v1"
 
 
 def log(msg: str) -> None:
@@ -222,7 +222,9 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(workload) if world == 1 else None,
-                "kernel": "spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue (split layout, 16 column classes)",
+                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue (split layout, {info.get('classes')} "
+                           "column classes, run per XCD in phases)" if info.get("classes", 1) > 1
+                           else "spmv pass: k_spmv_units (fused layout)"),
                 "classes": info.get("classes"),
                 "bytes_model": "12*E'_part + 36*V_part per launch (pull-fp64-v1)",
                 "spmv_ms_mean": round(spmv_ms, 4),

@@ -476,7 +476,12 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 static int class_setting() {
   int c = kClasses;
   if (const char *e = getenv("PR_CLASSES")) c = atoi(e);
-  return (c == 8 || c == 32) ? c : 16;
+  return (c == 8 || c == 16) ? c : 32;
+}
+
+static bool hot_phased_setting() {
+  const char *e = getenv("PR_HOT_PHASED");  // tuning knob
+  return e ? atoi(e) != 0 : true;
 }
 
 static int hot_slots_setting() {
@@ -754,6 +759,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
     g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
+    g->hot_phased = hot_phased_setting();
     PR_TRY(prepare_hot_kernel());
     const size_t nu = wp.units.size();
     g->n_hunits = (int64_t)nu;

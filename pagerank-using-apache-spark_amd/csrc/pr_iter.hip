@@ -151,14 +151,17 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }  // namespace
 
 int prepare_hot_kernel() {
-  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return PR_OK;
 }
 
 int launch_hot(pr_graph *g, int in) {
   const size_t lds = g->hot.lds_bytes();
-  hipLaunchKernelGGL((k_spmv_hot<0, 0>), dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
+  auto *kern = g->hot_phased ? &k_spmv_hot<0, 0, 1> : &k_spmv_hot<0, 0, 0>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
                      g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),

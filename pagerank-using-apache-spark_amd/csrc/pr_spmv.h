@@ -394,32 +394,19 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   }
 }
 
-template <int ORDER = 0, int DIAG = 0>
-__global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
-                                                          const int64_t *__restrict__ ucum, HotGeom hg,
-                                                          const uint32_t *__restrict__ colh,
-                                                          const uint32_t *__restrict__ hmeta,
-                                                          const double *__restrict__ cin, uint32_t cin_bytes,
-                                                          double *__restrict__ partial,
-                                                          const int64_t *__restrict__ poff,
-                                                          double *__restrict__ piece_part,
-                                                          const int32_t *__restrict__ hpos) {
-  extern __shared__ double hot[];
-  // class x runs on XCD x % 8 (round-robin dispatch: workgroup b on XCD b % 8)
-  const int x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
-  const int team = (int)(blockIdx.x / hg.C), nteams = (int)(gridDim.x / hg.C);
-  // stage the class's hot contributions (the previous iteration's, final before this launch)
-  const int nh = hg.P * hg.Kp;
-  const int32_t *hp = hpos + (int64_t)x * nh;
-  for (int i = threadIdx.x; i < nh; i += kHotThreads) hot[1 + i] = cin[hp[i]];
-  if (threadIdx.x == 0) hot[0] = 0.0;
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+// One class's wave units, strided over `nteams` workgroups (this one is `team`), with the
+// class's hot set already in LDS.
+template <int ORDER, int DIAG>
+__device__ __forceinline__ void hot_class_units(int x, int team, int nteams, const Unit *__restrict__ units,
+                                                const int64_t *__restrict__ ucum, const HotGeom &hg,
+                                                const uint32_t *__restrict__ colh,
+                                                const uint32_t *__restrict__ hmeta, const double *hot,
+                                                __amdgpu_buffer_rsrc_t crs, double *__restrict__ partial,
+                                                const int64_t *__restrict__ poff, double *__restrict__ piece_part,
+                                                double *stage, int wv) {
   const int64_t p0 = poff[x];
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)(partial + p0), 0, (uint32_t)((poff[x + 1] - p0) * 8), 0x00020000);
-  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
-  double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int64_t beg = ucum[x], end = ucum[x + 1];
   const int64_t stride = (int64_t)nteams * (kHotThreads / kWave);
   int64_t k = beg + (int64_t)team * (kHotThreads / kWave) + wv;
@@ -457,6 +444,49 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
       k += stride;
       if (k >= end) return;
     }
+  }
+}
+
+// The class units of the split layout, one 1024-thread workgroup per CU.  Round-robin dispatch
+// puts workgroup b on XCD b % 8; XCD k owns classes k, k + 8, ...  PHASED = 0: the XCD's
+// workgroups are split between its classes, all running at once.  PHASED = 1: all of the XCD's
+// workgroups run its classes one after another, so its L2 holds one class's sources at a time
+// (1/C of the gather space instead of 8/C); the hot set is restaged per class.
+template <int ORDER = 0, int DIAG = 0, int PHASED = 0>
+__global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
+                                                          const int64_t *__restrict__ ucum, HotGeom hg,
+                                                          const uint32_t *__restrict__ colh,
+                                                          const uint32_t *__restrict__ hmeta,
+                                                          const double *__restrict__ cin, uint32_t cin_bytes,
+                                                          double *__restrict__ partial,
+                                                          const int64_t *__restrict__ poff,
+                                                          double *__restrict__ piece_part,
+                                                          const int32_t *__restrict__ hpos) {
+  extern __shared__ double hot[];
+  const int nh = hg.P * hg.Kp;
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
+  const int n_phase = PHASED ? hg.C / kXcds : 1;
+  for (int ph = 0; ph < n_phase; ++ph) {
+    int x, team, nteams;
+    if constexpr (PHASED) {
+      x = (int)(blockIdx.x % kXcds) + kXcds * ph;
+      team = (int)(blockIdx.x / kXcds);
+      nteams = (int)(gridDim.x / kXcds);
+      if (ph > 0) __syncthreads();  // every wave is done with the previous class's hot set
+    } else {
+      x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
+      team = (int)(blockIdx.x / hg.C);
+      nteams = (int)(gridDim.x / hg.C);
+    }
+    // stage the class's hot contributions (the previous iteration's, final before this launch)
+    const int32_t *hp = hpos + (int64_t)x * nh;
+    for (int i = threadIdx.x; i < nh; i += kHotThreads) hot[1 + i] = cin[hp[i]];
+    if (threadIdx.x == 0) hot[0] = 0.0;
+    __syncthreads();
+    hot_class_units<ORDER, DIAG>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,
+                                 piece_part, stage, wv);
   }
 }
 

@@ -267,6 +267,7 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
     take k_spmv_hot's gather-space loads instead of the LDS -- the path every large graph uses --
     with hub segments split into pieces, empty (row, class) pairs and several parts."""
     monkeypatch.setenv("PR_HOT_SLOTS", str(slots))
+    monkeypatch.setenv("PR_CLASSES", "16")  # 16 classes: segments long enough to need pieces
     rng = np.random.default_rng(40 + slots)
     V = 30000
     src, dst = random_edges(rng, V, 400000, hub_frac=0.03)
@@ -283,6 +284,22 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
     finally:
         for p in parts:
             p.close()
+
+
+@pytest.mark.parametrize("classes,phased", [(8, "0"), (16, "0"), (16, "1"), (32, "0")])
+def test_split_class_schedules(hip, oracle_c, classes, phased, monkeypatch):
+    """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
+    after another with the hot set restaged per class); the default is 32 classes, phased."""
+    monkeypatch.setenv("PR_CLASSES", str(classes))
+    monkeypatch.setenv("PR_HOT_PHASED", phased)
+    monkeypatch.setenv("PR_HOT_SLOTS", "300")
+    rng = np.random.default_rng(90 + classes)
+    V = 50000
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.03)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 6, layout="split")
+    assert info["classes"] == classes
+    for it in range(6):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
 def test_rmat_s20_split_default_hot_set(hip, oracle_c):

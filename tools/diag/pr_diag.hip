@@ -182,7 +182,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 4>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 5>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 6>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 8>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 9>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 10>),
@@ -191,7 +191,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 4>)};
-  if (variant < 0 || variant > 15 || variant == 7) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 15) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
