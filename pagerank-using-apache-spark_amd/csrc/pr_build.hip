@@ -727,6 +727,12 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     keys.reset();
     tmp.reset();
     for (int x = C; x < kMaxClasses; ++x) poff[x + 1] = poff[x];
+    // absolute first slots when every partial has a 32-bit byte offset (k_epilogue<C, true>)
+    g->epi_abs = poff[C] < (int64_t(1) << 29) - 1;
+    if (const char *e = getenv("PR_EPI_ABS")) g->epi_abs = g->epi_abs && atoi(e) != 0;  // A/B knob
+    if (g->epi_abs)
+      for (int64_t blk = 0; blk < g->nblk; ++blk)
+        for (int x = 0; x < C; ++x) hbase[(size_t)blk * C + x] += (int32_t)poff[x];
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
@@ -760,6 +766,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
     g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
     g->hot_phased = hot_phased_setting();
+
     PR_TRY(prepare_hot_kernel());
     const size_t nu = wp.units.size();
     g->n_hunits = (int64_t)nu;

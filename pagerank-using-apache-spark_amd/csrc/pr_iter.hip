@@ -224,7 +224,9 @@ int iter_compute(pr_graph *g) {
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
-    hipLaunchKernelGGL(g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>), dim3(g->ep_blocks),
+    auto *epi = g->epi_abs ? (g->C == 32 ? k_epilogue<32, true> : (g->C == 16 ? k_epilogue<16, true> : k_epilogue<8, true>))
+                           : (g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>));
+    hipLaunchKernelGGL(epi, dim3(g->ep_blocks),
                        dim3(kThreads), 0, s, g->nblk, g->part_off, g->partial.as<double>(),
                        g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(),
                        g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,

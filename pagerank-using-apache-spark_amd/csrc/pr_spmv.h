@@ -510,7 +510,9 @@ __global__ __launch_bounds__(kThreads) void k_seg_reduce(int64_t n_seg, const in
 // sums in class order (row L's class-x slot = cbase[blk][x] + rows of the block before L that
 // have class-x in-links: one ballot), the in-degree-0 quirk, then the fused update of
 // k_spmv_units (r' without FMA, c' = r'/d, dangling and L1 partials).
-template <int C>
+// ABS: cbase holds absolute slot indices (all classes' partials < 2^29 slots): one buffer
+// resource over the whole partial array instead of one per class (which spills SGPRs).
+template <int C, bool ABS = false>
 __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po, const double *__restrict__ partial,
                                                        const uint32_t *__restrict__ rmask,
                                                        const int32_t *__restrict__ cbase,
@@ -540,10 +542,16 @@ __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po,
       const bool has = (m >> x) & 1u;
       const unsigned long long bal = __ballot(has);
       const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(partial + po.o[x]), 0, (uint32_t)((po.o[x + 1] - po.o[x]) * 8), 0x00020000);
       const uint32_t off = has ? ((uint32_t)cb[x] + (uint32_t)pre) * 8u : 0xFFFFFFF8u;
-      v[x] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(prs, off, 0, 2));
+      if constexpr (ABS) {
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)partial, 0, (uint32_t)(po.o[C] * 8), 0x00020000);
+        v[x] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(prs, off, 0, 2));
+      } else {
+        const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(partial + po.o[x]), 0, (uint32_t)((po.o[x + 1] - po.o[x]) * 8), 0x00020000);
+        v[x] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(prs, off, 0, 2));
+      }
     }
     double S = 0.0;
 #pragma unroll

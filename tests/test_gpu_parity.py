@@ -286,12 +286,16 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
             p.close()
 
 
-@pytest.mark.parametrize("classes,phased", [(8, "0"), (16, "0"), (16, "1"), (32, "0")])
-def test_split_class_schedules(hip, oracle_c, classes, phased, monkeypatch):
+@pytest.mark.parametrize("classes,phased,epi_abs", [(8, "0", "1"), (16, "0", "0"), (16, "1", "1"), (32, "0", "0"),
+                                                     (32, "1", "0")])
+def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, monkeypatch):
     """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
-    after another with the hot set restaged per class); the default is 32 classes, phased."""
+    after another with the hot set restaged per class) and both epilogue slot addressings (one
+    buffer over all partials, or one per class for > 2^29 slots); the default is 32 classes,
+    phased, absolute slots."""
     monkeypatch.setenv("PR_CLASSES", str(classes))
     monkeypatch.setenv("PR_HOT_PHASED", phased)
+    monkeypatch.setenv("PR_EPI_ABS", epi_abs)
     monkeypatch.setenv("PR_HOT_SLOTS", "300")
     rng = np.random.default_rng(90 + classes)
     V = 50000
