@@ -473,10 +473,17 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 
 // Tuning knobs read at build time: column classes of the split layout (8 = one
 // per XCD, 16 = two per XCD) and the size of the LDS hot set.
-static int class_setting() {
-  int c = kClasses;
-  if (const char *e = getenv("PR_CLASSES")) c = atoi(e);
-  return (c == 8 || c == 16) ? c : 32;
+// Column classes of the split layout: the fewest (8, 16, 32) whose class region of the gather
+// space fits one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time), capped at
+// kMaxClasses; PR_CLASSES overrides.  R-MAT s26 (262 MB) -> 32, LiveJournal (39 MB) -> 16.
+static int class_setting(int64_t gather_bytes) {
+  if (const char *e = getenv("PR_CLASSES")) {
+    const int c = atoi(e);
+    return (c == 8 || c == 16) ? c : 32;
+  }
+  for (int c = kXcds; c < kMaxClasses; c *= 2)
+    if (gather_bytes <= (int64_t)c * kL2BytesPerXcd) return c;
+  return kMaxClasses;
 }
 
 static bool hot_phased_setting() {
@@ -491,7 +498,7 @@ static int hot_slots_setting() {
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
-  static_assert(kMaxClasses == 4 * kXcds && kClasses % kXcds == 0, "class counts");
+  static_assert(kMaxClasses == 4 * kXcds, "class counts");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -584,7 +591,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
   // Column classes when the gather space (every part's slice: the columns a part reads) outgrows
   // the L2s (pr_graph.h).
-  const int c_split = class_setting();
+  const int c_split = class_setting((int64_t)P * g->n_local_max * 8);
   int C = ((int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
   if (g->flags & PR_LAYOUT_SPLIT) C = c_split;

@@ -92,7 +92,7 @@ __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
 constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
-constexpr int kClasses = 32;                         // default: four classes per XCD, run in phases
+constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
 constexpr int kMaxClasses = 32;                      // 8, 16 or 32 at run time (PR_CLASSES)
 constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather space outgrows the 8 x 4 MiB L2s
 
