@@ -740,6 +740,12 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     if (g->epi_abs)
       for (int64_t blk = 0; blk < g->nblk; ++blk)
         for (int x = 0; x < C; ++x) hbase[(size_t)blk * C + x] += (int32_t)poff[x];
+    // grouped epilogue: a sentinel row (block nblk) holds every class's end slot
+    g->epi_grp = g->epi_abs;
+    if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
+    if (g->epi_grp)
+      for (int x = 0; x < C; ++x) hbase.push_back((int32_t)poff[x + 1]);
+    if (const char *e = getenv("PR_EPI_WIN")) g->epi_win = atoi(e) == 1024 ? 1024 : 2048;
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
@@ -784,7 +790,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->colh.alloc(sizeof(uint32_t) * (wp.len > 0 ? wp.len : 8)));
     PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
     PR_TRY(g->cbase.alloc(sizeof(int32_t) * (hbase.size() + 1)));
-    PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] > 0 ? poff[C] : 1)));
+    // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
+    PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
     g->n_slots = poff[C];
     for (int x = 0; x <= kMaxClasses; ++x) g->part_off.o[x] = poff[x];
     PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
@@ -843,7 +850,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
-  g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
+  if (C > 1 && g->epi_grp)
+    g->ep_blocks = (int)grid_for((g->nblk + kEpiGroup - 1) / kEpiGroup, kEpiThreads / kWave, 2048);
+  else
+    g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
   // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));

@@ -95,6 +95,12 @@ constexpr int kXcds = 8;                             // XCDs of the MI355X (one 
 constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
 constexpr int kMaxClasses = 32;                      // 8, 16 or 32 at run time (PR_CLASSES)
 constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather space outgrows the 8 x 4 MiB L2s
+// Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
+// their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
+constexpr int kEpiGroup = 8;
+constexpr int kEpiWin = 2048;         // 16 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
+constexpr int kEpiThreads = 256;      // 4 waves, 64 KiB of LDS: two workgroups per CU
+static_assert(kEpiWin >= 64 * kEpiGroup + 2, "one class run of a group must fit the window");
 
 // per-row info word: out-degree | flags
 constexpr uint32_t kRowDegMask = (1u << 28) - 1;

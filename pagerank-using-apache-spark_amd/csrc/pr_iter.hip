@@ -151,6 +151,15 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }  // namespace
 
 int prepare_hot_kernel() {
+  for (int w : {1024, 2048}) {
+    const int epi_lds = (int)(sizeof(double) * (kEpiThreads / kWave) * (w + 2));
+    const void *f8 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<8, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<8, 2048>);
+    const void *f16 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<16, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<16, 2048>);
+    const void *f32 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<32, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<32, 2048>);
+    PR_HIP(hipFuncSetAttribute(f8, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
+    PR_HIP(hipFuncSetAttribute(f16, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
+    PR_HIP(hipFuncSetAttribute(f32, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
+  }
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
@@ -224,6 +233,16 @@ int iter_compute(pr_graph *g) {
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
+    if (g->epi_grp) {
+      auto *epi = g->epi_win == 1024
+                      ? (g->C == 32 ? k_epilogue_grp<32, 1024> : (g->C == 16 ? k_epilogue_grp<16, 1024> : k_epilogue_grp<8, 1024>))
+                      : (g->C == 32 ? k_epilogue_grp<32, 2048> : (g->C == 16 ? k_epilogue_grp<16, 2048> : k_epilogue_grp<8, 2048>));
+      const size_t lds = sizeof(double) * (size_t)(kEpiThreads / kWave) * (g->epi_win + 2);
+      hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(kEpiThreads), lds, s, g->nblk, g->partial.as<double>(),
+                         g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                         g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
+                         (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);
+    } else {
     auto *epi = g->epi_abs ? (g->C == 32 ? k_epilogue<32, true> : (g->C == 16 ? k_epilogue<16, true> : k_epilogue<8, true>))
                            : (g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>));
     hipLaunchKernelGGL(epi, dim3(g->ep_blocks),
@@ -232,6 +251,7 @@ int iter_compute(pr_graph *g) {
                        g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
                        g->cbuf[in].as<double>(), g->slots, (double)g->V, g->teleport, g->damping,
                        g->unit_part.as<double2>() + g->n_units);
+    }
     n_parts += g->ep_blocks;
   }
   PR_HIP(hipGetLastError());

@@ -570,4 +570,103 @@ __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po,
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
+// Grouped epilogue (same arithmetic as k_epilogue, bitwise): the address unit charges per load
+// instruction, and k_epilogue spends C + 3 of them per 64-row block although a block's class-x
+// slots are only ~12 consecutive partials.  Here a wave takes G = kEpiGroup consecutive blocks.
+// For every class their slots are ONE contiguous run, [cbase[b0][x], cbase[b0 + G][x]) (class x's
+// segments are numbered in row order; cbase carries a sentinel row), so the wave copies whole
+// runs into its LDS window by LDS-DMA, 16 bytes per lane (128 slots per instruction: ~4 per
+// block instead of 35 at C = 32), as many classes at a time as the window holds.  Then, per
+// block and class in class order, one ballot gives the row's position in the staged run and the
+// row adds it from LDS.  Runs start at even slots (16-byte alignment): slot s of a run staged
+// at window offset f sits at f + s - (s & ~1).
+template <int C, int W = kEpiWin>
+__global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
+    int64_t nblk, const double *__restrict__ partial, const uint32_t *__restrict__ rmask,
+    const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
+    double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
+    double damping, double2 *__restrict__ ep_part) {
+  constexpr int G = kEpiGroup, NW = kEpiThreads / kWave;
+  static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
+  extern __shared__ double epi_lds[];  // NW windows of W slots, then NW double2 for the block sum
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  double *win = epi_lds + wv * W;
+  const double tdc = dc_from_slots(cin, sp) / n_vertices;
+  double dcp = 0.0, l1p = 0.0;
+  const int64_t ngrp = (nblk + G - 1) / G;
+  const int64_t nw = (int64_t)gridDim.x * NW;
+  for (int64_t gi = (int64_t)blockIdx.x * NW + wv; gi < ngrp; gi += nw) {
+    const int64_t b0 = gi * G;
+    const int nb = (int)min((int64_t)G, nblk - b0);
+    uint32_t m[G], info[G];
+    double rold[G], S[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t L = (b0 + g) * kWave + lane;
+      const bool ok = g < nb;
+      m[g] = ok ? rmask[L] : 0u;
+      info[g] = ok ? rowinfo[L] : kRowHole;
+      rold[g] = ok ? r[L] : 0.0;
+      S[g] = 0.0;
+    }
+    // lane x < C holds class x's run [cs, ce) (read back per class with v_readlane)
+    const int cs = lane < C ? cbase[b0 * C + lane] : 0;
+    const int ce = lane < C ? cbase[(b0 + nb) * C + lane] : 0;
+    for (int x = 0; x < C;) {
+      // stage the runs of classes [x, xe) that fit the window (at least one always does)
+      int fill = 0, xe = x;
+      for (; xe < C; ++xe) {
+        const int sa = __builtin_amdgcn_readlane(cs, xe) & ~1, ea = (__builtin_amdgcn_readlane(ce, xe) + 1) & ~1;
+        if (xe > x && fill + (ea - sa) > W) break;
+        const double *src = partial + sa;
+        for (int o = 0; o < ea - sa; o += 2 * kWave)
+          if (o + 2 * lane < ea - sa)
+            __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
+        fill += ea - sa;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
+      fill = 0;
+      for (int y = x; y < xe; ++y) {
+        const int s = __builtin_amdgcn_readlane(cs, y), sa = s & ~1, ea = (__builtin_amdgcn_readlane(ce, y) + 1) & ~1;
+        int run = fill + (s - sa);
+        // all G reads in flight before the first add (every lane reads; absent rows discard it)
+        bool has[G];
+        double v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          has[g] = (m[g] >> y) & 1u;
+          const unsigned long long bal = __ballot(has[g]);
+          const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          v[g] = win[min(run + pre, W - 1)];
+          run += __popcll(bal);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g)  // absent classes add an exact +0 (S >= +0), as in k_epilogue
+          S[g] = __dadd_rn(S[g], has[g] ? v[g] : 0.0);
+        fill += ea - sa;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+      x = xe;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t L = (b0 + g) * kWave + lane;
+      double Sv = S[g];
+      if (m[g] == 0) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
+      const double rn = affine(Sv, tdc, teleport, damping);
+      if (!(info[g] & kRowHole)) {
+        r[L] = rn;
+        const uint32_t d = info[g] & kRowDegMask;
+        if (d > 0) cout[L] = __ddiv_rn(rn, (double)d);
+        else if (info[g] & kRowSink) dcp = __dadd_rn(dcp, rn);
+        l1p = __dadd_rn(l1p, fabs(rn - rold[g]));
+      }
+    }
+  }
+  double2 *red2 = reinterpret_cast<double2 *>(epi_lds + NW * W);
+  const double2 part = block_sum2<kEpiThreads>(make_double2(dcp, l1p), red2);
+  if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
+}
+
 }  // namespace pr
