@@ -745,7 +745,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
     if (g->epi_grp)
       for (int x = 0; x < C; ++x) hbase.push_back((int32_t)poff[x + 1]);
-    if (const char *e = getenv("PR_EPI_WIN")) g->epi_win = atoi(e) == 1024 ? 1024 : 2048;
+    if (const char *e = getenv("PR_EPI_VAR")) g->epi_var = std::min(std::max(atoi(e), 0), kNumEpiVariants - 1);
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
@@ -851,7 +851,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
   if (C > 1 && g->epi_grp)
-    g->ep_blocks = (int)grid_for((g->nblk + kEpiGroup - 1) / kEpiGroup, kEpiThreads / kWave, 2048);
+    g->ep_blocks = (int)grid_for((g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G,
+                                 kEpiThreads / kWave, 2048);
   else
     g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
   // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)

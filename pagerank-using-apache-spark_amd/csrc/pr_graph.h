@@ -69,7 +69,7 @@ struct pr_graph {
   bool hot_phased = false;  // an XCD's classes one after another (k_spmv_hot PHASED)
   bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
   bool epi_grp = false;     // epi_abs + a sentinel cbase row: k_epilogue_grp (LDS-staged class runs)
-  int epi_win = pr::kEpiWin;  // its LDS window per wave (slots): 1024 or 2048 (PR_EPI_WIN)
+  int epi_var = 0;          // its (group, window) variant, pr_spmv.h kEpiVariants (PR_EPI_VAR)
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
   pr::DevBuf cbuf[2];

@@ -98,9 +98,14 @@ constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather sp
 // Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
-constexpr int kEpiWin = 2048;         // 16 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
-constexpr int kEpiThreads = 256;      // 4 waves, 64 KiB of LDS: two workgroups per CU
-static_assert(kEpiWin >= 64 * kEpiGroup + 2, "one class run of a group must fit the window");
+constexpr int kEpiWin = 1024;         // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
+constexpr int kEpiThreads = 256;      // 4 waves, 32 KiB of LDS: five workgroups per CU
+// (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
+struct EpiVariant {
+  int G, W;
+};
+constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}};
+constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);
 
 // per-row info word: out-degree | flags
 constexpr uint32_t kRowDegMask = (1u << 28) - 1;

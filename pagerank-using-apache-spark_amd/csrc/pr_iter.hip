@@ -151,15 +151,10 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }  // namespace
 
 int prepare_hot_kernel() {
-  for (int w : {1024, 2048}) {
-    const int epi_lds = (int)(sizeof(double) * (kEpiThreads / kWave) * (w + 2));
-    const void *f8 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<8, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<8, 2048>);
-    const void *f16 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<16, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<16, 2048>);
-    const void *f32 = w == 1024 ? reinterpret_cast<const void *>(&k_epilogue_grp<32, 1024>) : reinterpret_cast<const void *>(&k_epilogue_grp<32, 2048>);
-    PR_HIP(hipFuncSetAttribute(f8, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
-    PR_HIP(hipFuncSetAttribute(f16, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
-    PR_HIP(hipFuncSetAttribute(f32, hipFuncAttributeMaxDynamicSharedMemorySize, epi_lds));
-  }
+  for (int v = 0; v < kNumEpiVariants; ++v)
+    for (int c : {8, 16, 32})
+      PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v)),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
@@ -234,10 +229,8 @@ int iter_compute(pr_graph *g) {
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
     if (g->epi_grp) {
-      auto *epi = g->epi_win == 1024
-                      ? (g->C == 32 ? k_epilogue_grp<32, 1024> : (g->C == 16 ? k_epilogue_grp<16, 1024> : k_epilogue_grp<8, 1024>))
-                      : (g->C == 32 ? k_epilogue_grp<32, 2048> : (g->C == 16 ? k_epilogue_grp<16, 2048> : k_epilogue_grp<8, 2048>));
-      const size_t lds = sizeof(double) * (size_t)(kEpiThreads / kWave) * (g->epi_win + 2);
+      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var);
+      const size_t lds = epi_grp_lds(g->epi_var);
       hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(kEpiThreads), lds, s, g->nblk, g->partial.as<double>(),
                          g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                          g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,

@@ -580,13 +580,13 @@ __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po,
 // block and class in class order, one ballot gives the row's position in the staged run and the
 // row adds it from LDS.  Runs start at even slots (16-byte alignment): slot s of a run staged
 // at window offset f sits at f + s - (s & ~1).
-template <int C, int W = kEpiWin>
+template <int C, int G = kEpiGroup, int W = kEpiWin>
 __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const uint32_t *__restrict__ rmask,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part) {
-  constexpr int G = kEpiGroup, NW = kEpiThreads / kWave;
+  constexpr int NW = kEpiThreads / kWave;
   static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
   extern __shared__ double epi_lds[];  // NW windows of W slots, then NW double2 for the block sum
   const int lane = lane_id();
@@ -668,5 +668,23 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
   const double2 part = block_sum2<kEpiThreads>(make_double2(dcp, l1p), red2);
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
+
+// k_epilogue_grp instantiations by variant (pr_internal.h kEpiVariants)
+using EpiGrpFn = void (*)(int64_t, const double *, const uint32_t *, const int32_t *, const uint32_t *, double *,
+                          double *, const double *, SlotPos, double, double, double, double2 *);
+template <int C>
+inline EpiGrpFn epi_grp_kernel_c(int var) {
+  switch (var) {
+    case 1: return k_epilogue_grp<C, kEpiVariants[1].G, kEpiVariants[1].W>;
+    case 2: return k_epilogue_grp<C, kEpiVariants[2].G, kEpiVariants[2].W>;
+    case 3: return k_epilogue_grp<C, kEpiVariants[3].G, kEpiVariants[3].W>;
+    case 4: return k_epilogue_grp<C, kEpiVariants[4].G, kEpiVariants[4].W>;
+    default: return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W>;
+  }
+}
+inline EpiGrpFn epi_grp_kernel(int C, int var) {
+  return C == 32 ? epi_grp_kernel_c<32>(var) : (C == 16 ? epi_grp_kernel_c<16>(var) : epi_grp_kernel_c<8>(var));
+}
+inline size_t epi_grp_lds(int var) { return sizeof(double) * (size_t)(kEpiThreads / kWave) * (kEpiVariants[var].W + 2); }
 
 }  // namespace pr

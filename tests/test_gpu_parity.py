@@ -289,19 +289,20 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
 @pytest.mark.parametrize("classes,phased,epi_abs,epi_grp", [(8, "0", "1", "1"), (16, "0", "0", "1"), (16, "1", "1", "0"),
                                                              (16, "1", "1", "1"), (32, "0", "0", "1"),
                                                              (32, "1", "1", "0"), (32, "1", "1", "1"),
-                                                             (32, "1", "1", "w1024")])
+                                                             (32, "1", "1", "v1"), (32, "1", "1", "v2"),
+                                                             (32, "1", "1", "v4")])
 def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp, monkeypatch):
     """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
     after another with the hot set restaged per class) and the three epilogues: grouped (class
     runs of 8 blocks staged in LDS; here ~10 segments per row, so a group's runs take several
     window loads), one load per class and block over all partials, or one buffer per class (the
-    > 2^29-slot path, which also turns the grouped one off); the grouped one with both LDS window
-    sizes.  Default: 32 classes, phased, grouped."""
+    > 2^29-slot path, which also turns the grouped one off); the grouped one in several (blocks
+    per group, LDS window) variants.  Default: 32 classes, phased, grouped."""
     monkeypatch.setenv("PR_CLASSES", str(classes))
     monkeypatch.setenv("PR_HOT_PHASED", phased)
     monkeypatch.setenv("PR_EPI_ABS", epi_abs)
     monkeypatch.setenv("PR_EPI_GRP", "0" if epi_grp == "0" else "1")
-    monkeypatch.setenv("PR_EPI_WIN", "1024" if epi_grp == "w1024" else "2048")
+    monkeypatch.setenv("PR_EPI_VAR", epi_grp[1:] if epi_grp.startswith("v") else "0")
     monkeypatch.setenv("PR_HOT_SLOTS", "300")
     rng = np.random.default_rng(90 + classes)
     V = 50000
