@@ -400,12 +400,13 @@ __global__ void k_mark_ends(int64_t R, const int64_t *__restrict__ rp, int32_t *
 }
 
 // Row class masks: bit x when the row has a class-x in-link.
-__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, uint32_t *__restrict__ rmask) {
+template <class M>
+__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, M *__restrict__ rmask) {
   for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t m = 0;
+    M m = 0;
     for (int x = 0; x < C; ++x) {
       const int64_t *rp = rp_all + (int64_t)x * (R + 1);
-      if (rp[L + 1] > rp[L]) m |= 1u << x;
+      if (rp[L + 1] > rp[L]) m |= M(1) << x;
     }
     rmask[L] = m;
   }
@@ -473,17 +474,17 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 
 // Tuning knobs read at build time: column classes of the split layout (8 = one
 // per XCD, 16 = two per XCD) and the size of the LDS hot set.
-// Column classes of the split layout: the fewest (8, 16, 32) whose class region of the gather
+// Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the gather
 // space fits one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time), capped at
-// kMaxClasses; PR_CLASSES overrides.  R-MAT s26 (262 MB) -> 32, LiveJournal (39 MB) -> 16.
+// kAutoMaxClasses; PR_CLASSES overrides.  R-MAT s26 (262 MB) -> 64, LiveJournal (39 MB) -> 16.
 static int class_setting(int64_t gather_bytes) {
   if (const char *e = getenv("PR_CLASSES")) {
     const int c = atoi(e);
-    return (c == 8 || c == 16) ? c : 32;
+    return (c == 8 || c == 16 || c == 64) ? c : 32;
   }
-  for (int c = kXcds; c < kMaxClasses; c *= 2)
+  for (int c = kXcds; c < kAutoMaxClasses; c *= 2)
     if (gather_bytes <= (int64_t)c * kL2BytesPerXcd) return c;
-  return kMaxClasses;
+  return kAutoMaxClasses;
 }
 
 static bool hot_phased_setting() {
@@ -498,7 +499,7 @@ static int hot_slots_setting() {
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
-  static_assert(kMaxClasses == 4 * kXcds, "class counts");
+  static_assert(kMaxClasses == 8 * kXcds, "class counts");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -743,15 +744,22 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     // grouped epilogue: a sentinel row (block nblk) holds every class's end slot
     g->epi_grp = g->epi_abs;
     if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
+    if (C > 32 && !g->epi_grp) return fail(PR_ERR_INVALID, "64 column classes need the grouped epilogue (< 2^29 partial slots)");
     if (g->epi_grp)
       for (int x = 0; x < C; ++x) hbase.push_back((int32_t)poff[x + 1]);
     if (const char *e = getenv("PR_EPI_VAR")) g->epi_var = std::min(std::max(atoi(e), 0), kNumEpiVariants - 1);
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
-    PR_TRY(g->rmask.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
-    hipLaunchKernelGGL(k_row_masks, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
-                       g->rmask.as<uint32_t>());
+    if (C > 32) {
+      PR_TRY(g->rmask.alloc(sizeof(uint64_t) * ((size_t)R + 1)));
+      hipLaunchKernelGGL(k_row_masks<uint64_t>, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
+                         g->rmask.as<uint64_t>());
+    } else {
+      PR_TRY(g->rmask.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
+      hipLaunchKernelGGL(k_row_masks<uint32_t>, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
+                         g->rmask.as<uint32_t>());
+    }
     PR_HIP(hipGetLastError());
     rp_all.reset();
     if (wp.len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");

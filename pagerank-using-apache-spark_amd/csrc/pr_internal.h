@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "pagerank_hip.h"
@@ -93,7 +94,10 @@ __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
 constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
 constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
-constexpr int kMaxClasses = 32;                      // 8, 16 or 32 at run time (PR_CLASSES)
+constexpr int kMaxClasses = 64;                      // 8, 16, 32 or 64 at run time (PR_CLASSES)
+constexpr int kAutoMaxClasses = 64;                  // the most the size policy picks by itself
+// per-row class mask (rmask): 32 bits up to 32 classes, 64 bits at 64
+template <int C> using ClassMask = typename std::conditional<(C > 32), uint64_t, uint32_t>::type;
 constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather space outgrows the 8 x 4 MiB L2s
 // Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.

@@ -152,7 +152,7 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 
 int prepare_hot_kernel() {
   for (int v = 0; v < kNumEpiVariants; ++v)
-    for (int c : {8, 16, 32})
+    for (int c : {8, 16, 32, 64})
       PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v)),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),
@@ -232,7 +232,7 @@ int iter_compute(pr_graph *g) {
       const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var);
       const size_t lds = epi_grp_lds(g->epi_var);
       hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(kEpiThreads), lds, s, g->nblk, g->partial.as<double>(),
-                         g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                         g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                          g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                          (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);
     } else {

@@ -570,28 +570,54 @@ __global__ __launch_bounds__(kThreads) void k_epilogue(int64_t nblk, PartOff po,
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
-// Grouped epilogue (same arithmetic as k_epilogue, bitwise): the address unit charges per load
+// One class of a group in k_epilogue_grp: per block, one ballot of the rows with in-links of
+// the class (bit `bit` of their mask word) puts each such row at window slot run + (its rank among
+// them), counted straight into the mbcnt accumulator; the other rows read the window's zero slot.
+// All G reads are in flight before the first add; returns run past the group's slots.
+template <int G>
+__device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t bit, int run, const double *win,
+                                             int zslot, double (&S)[G]) {
+  double v[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const bool has = (mw[g] & bit) != 0u;
+    const unsigned long long bal = __ballot(has);
+    const int idx = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)run));
+    v[g] = win[has ? idx : zslot];
+    run += __popcll(bal);
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) S[g] = __dadd_rn(S[g], v[g]);  // absent: + (+0), exact since S >= +0
+  return run;
+}
+
+// Grouped epilogue (row sums bitwise those of k_epilogue): the address unit charges per load
 // instruction, and k_epilogue spends C + 3 of them per 64-row block although a block's class-x
 // slots are only ~12 consecutive partials.  Here a wave takes G = kEpiGroup consecutive blocks.
 // For every class their slots are ONE contiguous run, [cbase[b0][x], cbase[b0 + G][x]) (class x's
 // segments are numbered in row order; cbase carries a sentinel row), so the wave copies whole
 // runs into its LDS window by LDS-DMA, 16 bytes per lane (128 slots per instruction: ~4 per
-// block instead of 35 at C = 32), as many classes at a time as the window holds.  Then, per
-// block and class in class order, one ballot gives the row's position in the staged run and the
-// row adds it from LDS.  Runs start at even slots (16-byte alignment): slot s of a run staged
-// at window offset f sits at f + s - (s & ~1).
+// block instead of 35 at C = 32), as many classes at a time as the window holds; classes without
+// slots in the group are skipped.  Then, per class in class order and block, one ballot gives the
+// row's position in the staged run and the row adds it from LDS (epi_class_add).  Runs start at
+// even slots (16-byte alignment): slot s of a run staged at window offset f sits at
+// f + s - (s & ~1).  Each wave's window is W slots plus a zero slot (and one of padding).
 template <int C, int G = kEpiGroup, int W = kEpiWin>
 __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
-    int64_t nblk, const double *__restrict__ partial, const uint32_t *__restrict__ rmask,
+    int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part) {
   constexpr int NW = kEpiThreads / kWave;
+  using M = ClassMask<C>;
+  const M *__restrict__ rmask = static_cast<const M *>(rmask_v);
   static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
-  extern __shared__ double epi_lds[];  // NW windows of W slots, then NW double2 for the block sum
+  extern __shared__ double epi_lds[];  // NW windows of W + 2 slots, then NW double2 for the block sum
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
-  double *win = epi_lds + wv * W;
+  double *win = epi_lds + wv * (W + 2);
+  if (lane == 0) win[W] = 0.0;  // the zero slot (never a DMA target: fill <= W)
   const double tdc = dc_from_slots(cin, sp) / n_vertices;
   double dcp = 0.0, l1p = 0.0;
   const int64_t ngrp = (nblk + G - 1) / G;
@@ -599,13 +625,15 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
   for (int64_t gi = (int64_t)blockIdx.x * NW + wv; gi < ngrp; gi += nw) {
     const int64_t b0 = gi * G;
     const int nb = (int)min((int64_t)G, nblk - b0);
-    uint32_t m[G], info[G];
+    uint32_t mlo[G], mhi[G], info[G];
     double rold[G], S[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int64_t L = (b0 + g) * kWave + lane;
       const bool ok = g < nb;
-      m[g] = ok ? rmask[L] : 0u;
+      const M mk = ok ? rmask[L] : M(0);
+      mlo[g] = (uint32_t)mk;
+      mhi[g] = (uint32_t)((uint64_t)mk >> 32);
       info[g] = ok ? rowinfo[L] : kRowHole;
       rold[g] = ok ? r[L] : 0.0;
       S[g] = 0.0;
@@ -617,34 +645,24 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       // stage the runs of classes [x, xe) that fit the window (at least one always does)
       int fill = 0, xe = x;
       for (; xe < C; ++xe) {
-        const int sa = __builtin_amdgcn_readlane(cs, xe) & ~1, ea = (__builtin_amdgcn_readlane(ce, xe) + 1) & ~1;
-        if (xe > x && fill + (ea - sa) > W) break;
+        const int s = __builtin_amdgcn_readlane(cs, xe), e = __builtin_amdgcn_readlane(ce, xe);
+        if (e == s) continue;  // no slots in this group
+        const int sa = s & ~1, n2 = ((e + 1) & ~1) - sa;
+        if (xe > x && fill + n2 > W) break;
         const double *src = partial + sa;
-        for (int o = 0; o < ea - sa; o += 2 * kWave)
-          if (o + 2 * lane < ea - sa)
-            __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
-        fill += ea - sa;
+        for (int o = 0; o < n2; o += 2 * kWave)
+          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
+        fill += n2;
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
       fill = 0;
       for (int y = x; y < xe; ++y) {
-        const int s = __builtin_amdgcn_readlane(cs, y), sa = s & ~1, ea = (__builtin_amdgcn_readlane(ce, y) + 1) & ~1;
-        int run = fill + (s - sa);
-        // all G reads in flight before the first add (every lane reads; absent rows discard it)
-        bool has[G];
-        double v[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          has[g] = (m[g] >> y) & 1u;
-          const unsigned long long bal = __ballot(has[g]);
-          const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          v[g] = win[min(run + pre, W - 1)];
-          run += __popcll(bal);
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g)  // absent classes add an exact +0 (S >= +0), as in k_epilogue
-          S[g] = __dadd_rn(S[g], has[g] ? v[g] : 0.0);
-        fill += ea - sa;
+        const int s = __builtin_amdgcn_readlane(cs, y), e = __builtin_amdgcn_readlane(ce, y);
+        if (e == s) continue;
+        const int sa = s & ~1;
+        if (C <= 32 || y < 32) epi_class_add<G>(mlo, 1u << (y & 31), fill + (s - sa), win, W, S);
+        else epi_class_add<G>(mhi, 1u << (y & 31), fill + (s - sa), win, W, S);
+        fill += ((e + 1) & ~1) - sa;
       }
       __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
       x = xe;
@@ -653,7 +671,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     for (int g = 0; g < G; ++g) {
       const int64_t L = (b0 + g) * kWave + lane;
       double Sv = S[g];
-      if (m[g] == 0) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
+      if ((mlo[g] | mhi[g]) == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
       const double rn = affine(Sv, tdc, teleport, damping);
       if (!(info[g] & kRowHole)) {
         r[L] = rn;
@@ -664,13 +682,13 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       }
     }
   }
-  double2 *red2 = reinterpret_cast<double2 *>(epi_lds + NW * W);
+  double2 *red2 = reinterpret_cast<double2 *>(epi_lds + NW * (W + 2));
   const double2 part = block_sum2<kEpiThreads>(make_double2(dcp, l1p), red2);
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
 // k_epilogue_grp instantiations by variant (pr_internal.h kEpiVariants)
-using EpiGrpFn = void (*)(int64_t, const double *, const uint32_t *, const int32_t *, const uint32_t *, double *,
+using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
                           double *, const double *, SlotPos, double, double, double, double2 *);
 template <int C>
 inline EpiGrpFn epi_grp_kernel_c(int var) {
@@ -683,8 +701,9 @@ inline EpiGrpFn epi_grp_kernel_c(int var) {
   }
 }
 inline EpiGrpFn epi_grp_kernel(int C, int var) {
-  return C == 32 ? epi_grp_kernel_c<32>(var) : (C == 16 ? epi_grp_kernel_c<16>(var) : epi_grp_kernel_c<8>(var));
+  return C == 64 ? epi_grp_kernel_c<64>(var)
+                 : (C == 32 ? epi_grp_kernel_c<32>(var) : (C == 16 ? epi_grp_kernel_c<16>(var) : epi_grp_kernel_c<8>(var)));
 }
-inline size_t epi_grp_lds(int var) { return sizeof(double) * (size_t)(kEpiThreads / kWave) * (kEpiVariants[var].W + 2); }
+inline size_t epi_grp_lds(int var) { return sizeof(double) * (size_t)(kEpiThreads / kWave) * (kEpiVariants[var].W + 4); }
 
 }  // namespace pr

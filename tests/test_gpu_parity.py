@@ -43,7 +43,7 @@ def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, lay
     ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
     with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout) as g:
         if layout != "auto":
-            assert g.info()["classes"] in ((1,) if layout == "fused" else (8, 16, 32))
+            assert g.info()["classes"] in ((1,) if layout == "fused" else (8, 16, 32, 64))
         assert_csr_equal(g, csr)
         hist = []
         ranks, stats = g.run(iters, init_ranks=init, want_ranks_in_callback=True,
@@ -290,7 +290,8 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
                                                              (16, "1", "1", "1"), (32, "0", "0", "1"),
                                                              (32, "1", "1", "0"), (32, "1", "1", "1"),
                                                              (32, "1", "1", "v1"), (32, "1", "1", "v2"),
-                                                             (32, "1", "1", "v4")])
+                                                             (32, "1", "1", "v4"), (64, "0", "1", "1"),
+                                                             (64, "1", "1", "1"), (64, "1", "1", "v2")])
 def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp, monkeypatch):
     """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
     after another with the hot set restaged per class) and the three epilogues: grouped (class
