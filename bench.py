@@ -179,7 +179,7 @@ def main() -> int:
     gteps = n_edges / (ms_step * 1e-3) / 1e9
 
     # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot per column class,
-    # k_seg_reduce for long segments, k_epilogue over all rows) -- on this rank
+    # k_seg_reduce for long segments, k_epilogue_grp / k_epilogue over all rows) -- on this rank
     spmv_ms = st["spmv_ms_mean"]
     bytes_launch = 12 * info["local_edges"] + 36 * info["local_rows"]
     achieved = bytes_launch / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
@@ -222,7 +222,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(workload) if world == 1 else None,
-                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue (split layout, {info.get('classes')} "
+                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue[_grp] (split layout, {info.get('classes')} "
                            "column classes, run per XCD in phases)" if info.get("classes", 1) > 1
                            else "spmv pass: k_spmv_units (fused layout)"),
                 "classes": info.get("classes"),
