@@ -472,8 +472,7 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
   }
 }
 
-// Tuning knobs read at build time: column classes of the split layout (8 = one
-// per XCD, 16 = two per XCD) and the size of the LDS hot set.
+// Tuning knobs read at build time.
 // Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the gather
 // space fits one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time), capped at
 // kAutoMaxClasses; PR_CLASSES overrides.  R-MAT s26 (262 MB) -> 64, LiveJournal (39 MB) -> 16.
@@ -858,9 +857,12 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
-  if (C > 1 && g->epi_grp)
+  if (C > 1 && g->epi_grp) {
+    int cap = 2048;
+    if (const char *e = getenv("PR_EPI_BLOCKS")) cap = std::max(atoi(e), 1);  // A/B knob
     g->ep_blocks = (int)grid_for((g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G,
-                                 kEpiThreads / kWave, 2048);
+                                 kEpiThreads / kWave, cap);
+  }
   else
     g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
   // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)

@@ -108,7 +108,7 @@ constexpr int kEpiThreads = 256;      // 4 waves, 32 KiB of LDS: five workgroups
 struct EpiVariant {
   int G, W;
 };
-constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}};
+constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016}};
 constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);
 
 // per-row info word: out-degree | flags

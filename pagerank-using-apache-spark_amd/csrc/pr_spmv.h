@@ -697,6 +697,7 @@ inline EpiGrpFn epi_grp_kernel_c(int var) {
     case 2: return k_epilogue_grp<C, kEpiVariants[2].G, kEpiVariants[2].W>;
     case 3: return k_epilogue_grp<C, kEpiVariants[3].G, kEpiVariants[3].W>;
     case 4: return k_epilogue_grp<C, kEpiVariants[4].G, kEpiVariants[4].W>;
+    case 5: return k_epilogue_grp<C, kEpiVariants[5].G, kEpiVariants[5].W>;
     default: return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W>;
   }
 }
