@@ -103,7 +103,7 @@ constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather sp
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
 constexpr int kEpiWin = 1024;         // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
-constexpr int kEpiThreads = 256;      // 4 waves, 32 KiB of LDS: five workgroups per CU
+constexpr int kEpiThreads = 256;      // 4 waves, 32.1 KiB of LDS: four workgroups per CU
 // (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
 struct EpiVariant {
   int G, W;
@@ -137,11 +137,15 @@ constexpr uint32_t kEntZero = 0u;  // LDS slot 0
 constexpr uint32_t kMetaStep0 = 1u << 8;
 constexpr int kMetaExclShift = 14;
 // LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part),
-// then one staging window of kStageSlots segment sums per wave (32 KiB in all).
-constexpr int kStageSlots = 256;
+// then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
+// ~0.5 % and 64 by ~0.8 % at R-MAT s26, profiles/r01/stage_ab/).
+#ifndef PR_STAGE_SLOTS
+#define PR_STAGE_SLOTS 128  // other values: A/B builds only (tools/gpu/stage.sh)
+#endif
+constexpr int kStageSlots = PR_STAGE_SLOTS;
 constexpr int kHotLdsBytes = 160 * 1024;
 constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 2;
-constexpr int kHotSlotsDefault = kHotSlotsMax;  // 16382 hot contributions (128 KiB)
+constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18430 hot contributions (144 KiB)
 
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {

@@ -316,7 +316,7 @@ def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp,
 
 def test_rmat_s20_split_default_hot_set(hip, oracle_c):
     """BASELINE.json configs[0] (R-MAT scale 20, edge factor 16, 10 iterations) at full size
-    through the product layout: 16 classes of ~40 K rows, so the 16 K-slot hot set covers only
+    through the product layout: 16 classes of ~40 K rows, so the 18 K-slot hot set covers only
     the top of each class and both gather paths carry real traffic."""
     import torch
 
