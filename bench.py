@@ -89,6 +89,8 @@ def main() -> int:
     ap.add_argument("--graph", choices=["rmat", "er", "lj", "twitter"], default="rmat",
                     help="lj / twitter: the Chung-Lu shapes of BASELINE.json configs[1] / [4]")
     ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--layout", choices=["auto", "fused", "split"], default="auto",
+                    help="graph layout (A/B; auto picks by gather-space size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     a = ap.parse_args()
@@ -141,7 +143,8 @@ def main() -> int:
     log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
     want_cpu = (rank == 0 and world == 1 and not a.no_cpu_baseline)
     g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device=dev, device_input=True,
-                                 n_edges=E, part=rank, n_parts=world, keep_canonical=want_cpu)
+                                 n_edges=E, part=rank, n_parts=world, keep_canonical=want_cpu,
+                                 layout=a.layout)
     del s, d
     torch.cuda.empty_cache()
     info = g.info()

@@ -474,15 +474,16 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 
 // Tuning knobs read at build time.
 // Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the gather
-// space fits one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time), capped at
-// kAutoMaxClasses; PR_CLASSES overrides.  R-MAT s26 (262 MB) -> 64, LiveJournal (39 MB) -> 16.
+// space fits 3/4 of one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time; the
+// rest of the L2 carries the streamed codes and metadata), capped at kAutoMaxClasses; PR_CLASSES
+// overrides.  R-MAT s26 (262 MB) -> 64, ER s24 (134 MB) -> 64, LiveJournal (39 MB) -> 16.
 static int class_setting(int64_t gather_bytes) {
   if (const char *e = getenv("PR_CLASSES")) {
     const int c = atoi(e);
     return (c == 8 || c == 16 || c == 64) ? c : 32;
   }
   for (int c = kXcds; c < kAutoMaxClasses; c *= 2)
-    if (gather_bytes <= (int64_t)c * kL2BytesPerXcd) return c;
+    if (gather_bytes * 4 <= (int64_t)c * kL2BytesPerXcd * 3) return c;
   return kAutoMaxClasses;
 }
 
