@@ -98,7 +98,9 @@ constexpr int kMaxClasses = 64;                      // 8, 16, 32 or 64 at run t
 constexpr int kAutoMaxClasses = 64;                  // the most the size policy picks by itself
 // per-row class mask (rmask): 32 bits up to 32 classes, 64 bits at 64
 template <int C> using ClassMask = typename std::conditional<(C > 32), uint64_t, uint32_t>::type;
-constexpr int64_t kSplitMinSliceBytes = 32ll << 20;  // split once the gather space outgrows the 8 x 4 MiB L2s
+// split once the gather space passes 4 MiB: R-MAT s20 (5.2 MB, L2-resident either way) runs the
+// split layout at 8 classes in 0.09 ms/iter against 0.18 ms fused (profiles/r01/configs_ab/s20_*)
+constexpr int64_t kSplitMinSliceBytes = 4ll << 20;
 // Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
