@@ -855,7 +855,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)g->gsize));
     PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)g->gsize, s));
   }
-  g->fin_blocks = 512;
+  // k_finalize: one wave per long row, at least 16 workgroups (4096 threads for the <= 2048 block
+  // partials), at most 512
+  g->fin_blocks = (int)std::min<int64_t>(512, std::max<int64_t>(16, (g->n_long + kThreads / kWave - 1) / (kThreads / kWave)));
   PR_TRY(g->fin_part.alloc(sizeof(double) * 2 * g->fin_blocks));
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
