@@ -3,23 +3,27 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale 26] [--graph rmat|er|lj|twitter]
 
 A step is one PageRank iteration (Sparky.java:189-235) over the whole graph, inputs resident
-in HBM.  The graph is generated on the GPU (seeded R-MAT, Graph500 a/b/c = .57/.19/.19,
-edge factor 16), interned in first-appearance order (pr_intern_device) and built by
-libpagerank_hip; none of that is timed.  N > 1: launched by torch.distributed.run, one process
-per GPU; every rank builds its row part of the same graph and the parts exchange contributions
-with one RCCL all-gather per iteration (inside the library).  value = E' (distinct edges of
-the whole graph) / (max-over-ranks time per step) / 1e9.
+in HBM.  The graph is generated on the GPU (sparky_hip.workloads: seeded R-MAT, Graph500
+a/b/c = .57/.19/.19, edge factor 16), interned in first-appearance order (pr_intern_device) and
+built by libpagerank_hip; none of that is timed.  N > 1: launched by torch.distributed.run, one
+process per GPU; every rank builds its row part of the same graph and the parts exchange the
+contributions each one reads with grouped RCCL send/recv per iteration (inside the library).
+value = E' (distinct edges of the whole graph) / (max-over-ranks time per step) / 1e9.
 
 Rank 0 prints ONE JSON line (the driver's contract), including
-  roofline:      algorithmic bytes per SpMV launch (12 E'_part + 36 V_part) divided by
-                 the launch's mean HIP-event time on the library's stream, vs 8 TB/s;
-  cpu_baseline:  oracle/pagerank_oracle.c (OpenMP restatement of the same semantics) timed on
-                 this host on a bounded sample (a few iterations of the same graph's CSR).
+  roofline:       algorithmic bytes per SpMV pass (12 E'_part + 36 V_part) divided
+                  by the pass's mean HIP-event time on the library's stream, vs 8 TB/s;
+  cpu_baseline:   oracle/pagerank_oracle.c (OpenMP restatement of the same semantics) on this
+                  host's cores (N = 1 only): the median of iterations 2..K of the same graph;
+  parity_max_rel: after the timed region, K iterations from a fresh reset on the GPU (every
+                  rank's rows summed into one vector on rank 0 when N > 1) against K iterations
+                  of the oracle on the exported canonical CSR -- the north-star 1e-9 bar.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -38,7 +42,7 @@ def log(msg: str) -> None:
 
 
 def pmc_traffic(workload: str):
-    """Per-launch HBM bytes of the SpMV kernel from a committed rocprofv3 PMC summary."""
+    """Per-pass HBM bytes of the SpMV kernels from a committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_spmv.json")
     if not os.path.exists(path):
         return None
@@ -52,31 +56,55 @@ def pmc_traffic(workload: str):
     return None
 
 
-def cpu_baseline(g, n_edges: int, n_vertices: int, budget_s: float):
+def host_cores():
+    """(candidate OpenMP thread counts, description): nproc, the affinity mask and the cgroup
+    CPU quota of this host -- the GPU box shows the whole machine in nproc but may grant a
+    share of it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(p)))
+    except (OSError, ValueError):
+        pass
+    cands = {aff}
+    if quota is not None:
+        cands.add(min(aff, quota))
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        cands.add(min(env, aff))
+    desc = f"nproc {nproc}, affinity {aff}, cgroup quota {quota if quota is not None else 'none'}"
+    return sorted(cands), desc
+
+
+def oracle_leg(g, V: int, iters: int, pick_threads: bool):
+    """K oracle iterations on the graph's exported canonical CSR (test infrastructure: the
+    checker and the CPU baseline, never the measured path).  Returns (result, threads, desc)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle_c
 
     oracle_c.build()
     ex = g.export_csr()
-    csr = oracle_c.CSR(n_vertices, ex.row_ptr, ex.col_idx, ex.out_deg, ex.vflags)
+    csr = oracle_c.CSR(V, ex.row_ptr, ex.col_idx, ex.out_deg, ex.vflags)
     del ex
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    t0 = time.perf_counter()
-    oracle_c.run(csr, 1, nthreads=threads)
-    t1 = time.perf_counter() - t0
-    iters = max(1, min(10, int(budget_s / max(t1, 1e-6))))
-    t0 = time.perf_counter()
-    oracle_c.run(csr, iters, nthreads=threads)
-    t = (time.perf_counter() - t0) / iters
-    return {
-        "value": n_edges / t / 1e9,
-        "unit": "GTEPS",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{iters} iteration(s) of the same graph's canonical CSR on {threads} OpenMP "
-                  f"threads (oracle/pagerank_oracle.c, Neumaier row sums); {t * 1e3:.1f} ms/iter",
-    }
+    cands, desc = host_cores()
+    threads = cands[-1]
+    if pick_threads and len(cands) > 1:  # one iteration per candidate, keep the fastest
+        best = None
+        for t in cands:
+            ms = oracle_c.run(csr, 1, nthreads=t)["iter_ms"][0]
+            log(f"oracle: 1 iteration on {t} threads: {ms:.1f} ms")
+            if best is None or ms < best[0]:
+                best = (ms, t)
+        threads = best[1]
+    res = oracle_c.run(csr, iters, nthreads=threads)
+    return res, threads, desc, csr.n_edges
 
 
 def main() -> int:
@@ -91,13 +119,15 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--layout", choices=["auto", "fused", "split"], default="auto",
                     help="graph layout (A/B; auto picks by gather-space size)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (no cpu_baseline, no parity)")
+    ap.add_argument("--parity-iters", type=int, default=10, help="K of the parity / cpu_baseline leg (Sparky.java:187)")
     a = ap.parse_args()
 
+    import numpy as np
     import torch
 
     import sparky_hip
+    from sparky_hip.workloads import generate
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,38 +144,15 @@ def main() -> int:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
 
     t0 = time.perf_counter()
-    if a.graph in ("rmat", "er"):
-        seed = a.seed if a.seed is not None else (2 if a.graph == "rmat" else 3)
-        E = a.edge_factor << a.scale
-        labels = 1 << a.scale
-    else:
-        pre = dict(sparky_hip.CHUNGLU_PRESETS[a.graph])
-        seed = a.seed if a.seed is not None else pre["seed"]
-        E = pre["n_edges"] + pre["n_nolink"]
-        labels = pre["n_labels"]
-    s = torch.empty(E, dtype=torch.int32, device="cuda")
-    d = torch.empty(E, dtype=torch.int32, device="cuda")
-    if a.graph == "rmat":
-        sparky_hip.gen_rmat(dev, a.scale, E, s.data_ptr(), d.data_ptr(), seed=seed)
-        workload = f"R-MAT scale-{a.scale} edge-factor {a.edge_factor} (Graph500 .57/.19/.19, seed {seed})"
-    elif a.graph == "er":
-        sparky_hip.gen_er(dev, a.scale, E, s.data_ptr(), d.data_ptr(), seed=seed)
-        workload = f"Erdos-Renyi scale-{a.scale} degree {a.edge_factor} (seed {seed})"
-    else:
-        sparky_hip.gen_chunglu(dev, pre["n_labels"], pre["n_edges"], s.data_ptr(), d.data_ptr(),
-                               gamma_out=pre["gamma_out"], v0_out=pre["v0_out"], gamma_in=pre["gamma_in"],
-                               v0_in=pre["v0_in"], src_frac=pre["src_frac"], n_nolink=pre["n_nolink"], seed=seed)
-        workload = (f"{'LiveJournal' if a.graph == 'lj' else 'Twitter-2010'}-shaped Chung-Lu "
-                    f"({pre['n_labels']} labels, {pre['n_edges']} edges + {pre['n_nolink']} link-less records, "
-                    f"gamma out/in {pre['gamma_out']}/{pre['gamma_in']}, seed {seed})")
-    V = sparky_hip.intern_device(dev, E, labels, s.data_ptr(), d.data_ptr())
+    wl = generate(a.graph, scale=a.scale, edge_factor=a.edge_factor, seed=a.seed, device=dev)
+    V, E, workload = wl.n_vertices, wl.n_edges, wl.description
     t_gen = time.perf_counter() - t0
     log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
-    want_cpu = (rank == 0 and world == 1 and not a.no_cpu_baseline)
-    g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device=dev, device_input=True,
-                                 n_edges=E, part=rank, n_parts=world, keep_canonical=want_cpu,
+    validate = not a.no_cpu_baseline
+    g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
+                                 n_edges=E, part=rank, n_parts=world, keep_canonical=(validate and rank == 0),
                                  layout=a.layout)
-    del s, d
+    del wl
     torch.cuda.empty_cache()
     info = g.info()
     log(f"rank {rank}: build {g.stats()['build_ms']:.0f} ms; info {info}")
@@ -177,22 +184,66 @@ def main() -> int:
     else:
         t_total = t_local
     st = g.stats()
+    g.set_timing(False)
     ms_step = t_total / max(a.steps, 1) * 1e3
     n_edges = info["n_edges"]
     gteps = n_edges / (ms_step * 1e-3) / 1e9
+    xchg_ms = [st["exchange_ms_mean"]]
+    if dist is not None:
+        xt = torch.tensor([st["exchange_ms_mean"]], dtype=torch.float64, device="cuda")
+        allx = [torch.zeros_like(xt) for _ in range(world)]
+        dist.all_gather(allx, xt)
+        xchg_ms = [float(x.item()) for x in allx]
 
     # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot per column class,
-    # k_seg_reduce for long segments, k_epilogue_grp / k_epilogue over all rows) -- on this rank
+    # k_seg_reduce for long segments, k_epilogue_grp over all rows) -- on this rank
     spmv_ms = st["spmv_ms_mean"]
     bytes_launch = 12 * info["local_edges"] + 36 * info["local_rows"]
     achieved = bytes_launch / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
 
-    cpu = None
-    if want_cpu:
-        try:
-            cpu = cpu_baseline(g, n_edges, V, a.cpu_budget_s)
-        except Exception as e:  # reported, never fatal for the GPU number
-            log(f"cpu baseline failed: {e!r}")
+    # ---- validation leg (after the timed region): K iterations from a fresh reset vs the oracle ----
+    cpu, parity = None, None
+    if validate:
+        K = a.parity_iters
+        g.reset()
+        g.step(K)
+        g.sync()
+        mine = np.zeros(V, np.float64)
+        g.ranks(mine)  # this rank's rows; the others stay 0
+        owned_once = True
+        if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
+            rt = torch.from_numpy(mine).cuda()
+            own = torch.from_numpy((mine != 0).astype(np.int32)).cuda()
+            dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
+            dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                mine = rt.cpu().numpy()
+                owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
+            del rt, own
+        if rank == 0:
+            try:
+                res, threads, desc, e_csr = oracle_leg(g, V, K, pick_threads=(world == 1))
+                ref = res["ranks"]
+                parity = {"iterations": K, "max_rel": float(np.max(np.abs(mine - ref) / ref)) if V else 0.0,
+                          "vs": "oracle/pagerank_oracle.c on the exported canonical CSR",
+                          "ranks_from": f"{world} rank(s)", "every_row_owned_once": owned_once}
+                if world == 1 and K >= 2:
+                    it_ms = res["iter_ms"][1:]
+                    med = float(np.median(it_ms))
+                    cpu = {
+                        "value": round(e_csr / (med * 1e-3) / 1e9, 4),
+                        "unit": "GTEPS",
+                        "cores": threads,
+                        "kind": "port",
+                        "sample": (f"median of iterations 2..{K} ({med:.1f} ms/iter) of the same graph's canonical "
+                                   f"CSR on {threads} OpenMP threads (oracle/pagerank_oracle.c, Neumaier row sums); "
+                                   f"host: {desc}"),
+                    }
+                log(f"parity: max_rel {parity['max_rel']:.3e} after {K} iterations")
+            except Exception as e:  # reported, never fatal for the GPU number
+                log(f"oracle leg failed: {e!r}")
+        if dist is not None:
+            dist.barrier()
     g.close()
 
     if rank == 0:
@@ -234,6 +285,9 @@ def main() -> int:
                 "iter_ms_mean_events": round(st["iter_ms_mean"], 4),
                 "exchange_ms_mean": round(st["exchange_ms_mean"], 4),
             },
+            "exchange_ms_per_rank": [round(x, 4) for x in xchg_ms] if world > 1 else None,
+            "parity_max_rel": None if parity is None else parity["max_rel"],
+            "parity": parity,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -68,7 +68,10 @@ extern "C" {
 #define PR_INFO_CLASSES 13     /* column classes of the layout (1 = fused single pass)     */
 #define PR_INFO_XCHG_SEND 14   /* doubles this part sends per iteration (P > 1)           */
 #define PR_INFO_XCHG_RECV 15   /* doubles this part receives per iteration (P > 1)        */
-#define PR_INFO_COUNT 16
+#define PR_INFO_PARTIAL_SLOTS 16 /* (row, column class) segment sums of the split layout     */
+#define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
+#define PR_INFO_EPILOGUE 18    /* 0 fused, 1 per-block, 2 per-class buffers, 3 grouped      */
+#define PR_INFO_COUNT 19
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

@@ -40,6 +40,10 @@ int32_t prh_java_double(double x, char *buf);
 int prh_write_part(const prh_edges *e, const char *dir, int32_t iter, const double *ranks);
 /* "<url> has rank: <r>." for every URL, to path (NULL = stdout). */
 int prh_write_has_rank(const prh_edges *e, const char *path, const double *ranks);
+/* Resume: ranks[id] from the "(url,rank)" lines of every dir/part-* file (a PageRank<i>
+   directory written by prh_write_part or by Sparky.java:237's saveAsTextFile).  Every URL of
+   the edge list must appear exactly once, and only those. */
+int prh_read_ranks(const prh_edges *e, const char *dir, double *ranks);
 void prh_free(prh_edges *e);
 
 #ifdef __cplusplus

@@ -35,7 +35,7 @@ def lib():
         L.orc_build.argtypes = [ctypes.c_int32, ctypes.c_int64, P, P, P, P, P, P, P]
         L.orc_build.restype = ctypes.c_int
         L.orc_run.argtypes = [ctypes.c_int32, P, P, P, P, ctypes.c_int32, ctypes.c_int32,
-                              ctypes.c_double, ctypes.c_double, P, P, P, P, P, ctypes.c_int32]
+                              ctypes.c_double, ctypes.c_double, P, P, P, P, P, ctypes.c_int32, P]
         L.orc_run.restype = ctypes.c_int
         L.orc_flag_bits.restype = ctypes.c_uint32
         _lib = L
@@ -77,14 +77,16 @@ def build_csr(n_vertices: int, src: np.ndarray, dst: np.ndarray) -> CSR:
 
 def run(csr: CSR, iterations: int, dangling_none: bool = False, teleport: float = 0.15,
         damping: float = 0.85, init=None, keep_history: bool = False, nthreads: int = 0):
-    """Returns dict(ranks, dc[iters], l1[iters], history[iters, V] or None)."""
+    """Returns dict(ranks, dc[iters], l1[iters], iter_ms[iters], history[iters, V] or None)."""
     V = csr.n_vertices
     ranks = np.zeros(max(V, 1), np.float64)
     dc = np.zeros(max(iterations, 1), np.float64)
     l1 = np.zeros(max(iterations, 1), np.float64)
+    ms = np.zeros(max(iterations, 1), np.float64)
     hist = np.zeros((iterations, V), np.float64) if keep_history else None
     init_a = None if init is None else np.ascontiguousarray(init, dtype=np.float64)
     lib().orc_run(V, _p(csr.row_ptr), _p(csr.col_idx), _p(csr.out_deg), _p(csr.vflags), iterations,
                   1 if dangling_none else 0, teleport, damping, _p(init_a), _p(ranks), _p(dc), _p(l1),
-                  _p(hist), nthreads)
-    return {"ranks": ranks[:V], "dc": dc[:iterations], "l1": l1[:iterations], "history": hist}
+                  _p(hist), nthreads, _p(ms))
+    return {"ranks": ranks[:V], "dc": dc[:iterations], "l1": l1[:iterations], "iter_ms": ms[:iterations],
+            "history": hist}

@@ -154,7 +154,9 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
                                     g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C,
-                                    xchg_volume(g, true), xchg_volume(g, false)};
+                                    xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
+                                    g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
+                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2))};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

@@ -399,16 +399,17 @@ __global__ void k_mark_ends(int64_t R, const int64_t *__restrict__ rp, int32_t *
   }
 }
 
-// Row class masks: bit x when the row has a class-x in-link.
-template <class M>
-__global__ void k_row_masks(int64_t R, int C, const int64_t *__restrict__ rp_all, M *__restrict__ rmask) {
+// Row class masks: bit x when the row has a class-x in-link (nw 32-bit words per row).
+__global__ void k_row_masks(int64_t R, int C, int nw, const int64_t *__restrict__ rp_all, uint32_t *__restrict__ rmask) {
   for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
-    M m = 0;
-    for (int x = 0; x < C; ++x) {
-      const int64_t *rp = rp_all + (int64_t)x * (R + 1);
-      if (rp[L + 1] > rp[L]) m |= M(1) << x;
+    for (int w = 0; w < nw; ++w) {
+      uint32_t m = 0;
+      for (int b = 0; b < 32 && 32 * w + b < C; ++b) {
+        const int64_t *rp = rp_all + (int64_t)(32 * w + b) * (R + 1);
+        if (rp[L + 1] > rp[L]) m |= 1u << b;
+      }
+      rmask[L * nw + w] = m;
     }
-    rmask[L] = m;
   }
 }
 
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
 static int class_setting(int64_t gather_bytes) {
   if (const char *e = getenv("PR_CLASSES")) {
     const int c = atoi(e);
-    return (c == 8 || c == 16 || c == 64) ? c : 32;
+    return (c == 8 || c == 16 || c == 64 || c == 128) ? c : 32;
   }
   for (int c = kXcds; c < kAutoMaxClasses; c *= 2)
     if (gather_bytes * 4 <= (int64_t)c * kL2BytesPerXcd * 3) return c;
@@ -499,7 +500,7 @@ static int hot_slots_setting() {
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
-  static_assert(kMaxClasses == 8 * kXcds, "class counts");
+  static_assert(kMaxClasses == 16 * kXcds, "class counts");
   auto t_start = std::chrono::steady_clock::now();
   hipStream_t s = g->stream;
   const int32_t V = g->V;
@@ -735,29 +736,31 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     keys.reset();
     tmp.reset();
     for (int x = C; x < kMaxClasses; ++x) poff[x + 1] = poff[x];
-    // absolute first slots when every partial has a 32-bit byte offset (k_epilogue<C, true>)
+    // k_epilogue<C, true>: one buffer resource over all partials, so every partial needs a 32-bit
+    // byte offset (< 2^29 slots).  k_epilogue_grp addresses partials through int32 absolute slot
+    // indices (< 2^31 slots: R-MAT s26 has ~2^28.1, a graph 7x its size still fits).
     g->epi_abs = poff[C] < (int64_t(1) << 29) - 1;
     if (const char *e = getenv("PR_EPI_ABS")) g->epi_abs = g->epi_abs && atoi(e) != 0;  // A/B knob
-    if (g->epi_abs)
+    g->epi_grp = poff[C] < (int64_t(1) << 31) - 4;
+    if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
+    if (C > 32 && !g->epi_grp) return fail(PR_ERR_INVALID, "more than 32 column classes need the grouped epilogue (< 2^31 partial slots)");
+    if (!g->epi_grp && !g->epi_abs && poff[C] >= (int64_t(1) << 31) - 4)
+      return fail(PR_ERR_INVALID, "more than 2^31 partial slots");
+    // absolute first slots (grouped epilogue or k_epilogue<C, true>)
+    if (g->epi_abs || g->epi_grp)
       for (int64_t blk = 0; blk < g->nblk; ++blk)
         for (int x = 0; x < C; ++x) hbase[(size_t)blk * C + x] += (int32_t)poff[x];
     // grouped epilogue: a sentinel row (block nblk) holds every class's end slot
-    g->epi_grp = g->epi_abs;
-    if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
-    if (C > 32 && !g->epi_grp) return fail(PR_ERR_INVALID, "64 column classes need the grouped epilogue (< 2^29 partial slots)");
     if (g->epi_grp)
       for (int x = 0; x < C; ++x) hbase.push_back((int32_t)poff[x + 1]);
     if (const char *e = getenv("PR_EPI_VAR")) g->epi_var = std::min(std::max(atoi(e), 0), kNumEpiVariants - 1);
     wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
     seg_p0.push_back((int32_t)pieces);
     for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
-    if (C > 32) {
-      PR_TRY(g->rmask.alloc(sizeof(uint64_t) * ((size_t)R + 1)));
-      hipLaunchKernelGGL(k_row_masks<uint64_t>, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
-                         g->rmask.as<uint64_t>());
-    } else {
-      PR_TRY(g->rmask.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
-      hipLaunchKernelGGL(k_row_masks<uint32_t>, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, rp_all.as<int64_t>(),
+    {
+      const int nw = (C + 31) / 32;
+      PR_TRY(g->rmask.alloc(sizeof(uint32_t) * (size_t)nw * ((size_t)R + 1)));
+      hipLaunchKernelGGL(k_row_masks, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, nw, rp_all.as<int64_t>(),
                          g->rmask.as<uint32_t>());
     }
     PR_HIP(hipGetLastError());

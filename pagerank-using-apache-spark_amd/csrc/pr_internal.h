@@ -94,10 +94,11 @@ __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
 constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
 constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
-constexpr int kMaxClasses = 64;                      // 8, 16, 32 or 64 at run time (PR_CLASSES)
+constexpr int kMaxClasses = 128;                     // 8, 16, 32, 64 or 128 at run time (PR_CLASSES)
 constexpr int kAutoMaxClasses = 64;                  // the most the size policy picks by itself
-// per-row class mask (rmask): 32 bits up to 32 classes, 64 bits at 64
-template <int C> using ClassMask = typename std::conditional<(C > 32), uint64_t, uint32_t>::type;
+// per-row class mask (rmask): ceil(C / 32) 32-bit words per row, class x in bit x % 32 of word
+// x / 32 (at 64 classes the two words are one little-endian u64)
+template <int C> constexpr int mask_words() { return (C + 31) / 32; }
 // split once the gather space passes 4 MiB: R-MAT s20 (5.2 MB, L2-resident either way) runs the
 // split layout at 8 classes in 0.09 ms/iter against 0.18 ms fused (profiles/r01/configs_ab/s20_*)
 constexpr int64_t kSplitMinSliceBytes = 4ll << 20;

@@ -152,7 +152,7 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 
 int prepare_hot_kernel() {
   for (int v = 0; v < kNumEpiVariants; ++v)
-    for (int c : {8, 16, 32, 64})
+    for (int c : {8, 16, 32, 64, 128})
       PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v)),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),

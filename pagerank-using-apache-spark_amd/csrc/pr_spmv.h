@@ -307,7 +307,8 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *_
 // DIAG (diagnostics library only; results wrong when != 0): 1 = every value from LDS (no
 // gather-space loads), 2 = no partial stores, 3 = non-temporal partial stores, 4 / 5 = every
 // gather-space load folded into the first 4 / 32 MiB (L2- / Infinity-Cache-resident), 6 =
-// exec-masked gathers, 8 = every gather instruction reads 512 contiguous bytes.
+// exec-masked gathers, 8 = every gather instruction reads 512 contiguous bytes, 13 = every value
+// from LDS plus an out-of-range buffer load per entry, 14 = no LDS reads (gathers only).
 template <int DIAG>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, __amdgpu_buffer_rsrc_t crs,
                                                  double (&v)[kWavePT]) {
@@ -316,10 +317,12 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
     const uint32_t c = w.c[j];
     const bool glob = (int32_t)c < 0;
     uint32_t la = glob ? 0u : c;
-    if constexpr (DIAG == 1) la = c & 0xFFF8u;
-    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    if constexpr (DIAG == 1 || DIAG == 13) la = c & 0xFFF8u;
+    double a = 0.0;
+    if constexpr (DIAG != 14) a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
     double b = 0.0;
     uint32_t go = c ^ kEntGlobal;  // LDS codes become offsets >= 2^31: out of range, no request
+    if constexpr (DIAG == 13) go = 0xFFFFFFF8u;  // every buffer load out of range (cost of the instruction)
     if constexpr (DIAG == 4) go = glob ? (go & 0x3FFFF8u) : go;   // every gather within 4 MiB
     if constexpr (DIAG == 5) go = glob ? (go & 0x1FFFFF8u) : go;  // every gather within 32 MiB
     if constexpr (DIAG == 8)  // every wave-instruction reads 512 contiguous bytes
@@ -610,8 +613,8 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part) {
   constexpr int NW = kEpiThreads / kWave;
-  using M = ClassMask<C>;
-  const M *__restrict__ rmask = static_cast<const M *>(rmask_v);
+  constexpr int MW = mask_words<C>();  // 32-bit mask words per row
+  static_assert(MW == 1 || MW == 2 || MW == 4, "mask words");
   static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
   extern __shared__ double epi_lds[];  // NW windows of W + 2 slots, then NW double2 for the block sum
   const int lane = lane_id();
@@ -625,15 +628,21 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
   for (int64_t gi = (int64_t)blockIdx.x * NW + wv; gi < ngrp; gi += nw) {
     const int64_t b0 = gi * G;
     const int nb = (int)min((int64_t)G, nblk - b0);
-    uint32_t mlo[G], mhi[G], info[G];
+    uint32_t mw[MW][G], info[G];
     double rold[G], S[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int64_t L = (b0 + g) * kWave + lane;
       const bool ok = g < nb;
-      const M mk = ok ? rmask[L] : M(0);
-      mlo[g] = (uint32_t)mk;
-      mhi[g] = (uint32_t)((uint64_t)mk >> 32);
+      if constexpr (MW == 4) {
+        const uint4 q = ok ? static_cast<const uint4 *>(rmask_v)[L] : make_uint4(0u, 0u, 0u, 0u);
+        mw[0][g] = q.x, mw[1][g] = q.y, mw[2][g] = q.z, mw[3][g] = q.w;
+      } else if constexpr (MW == 2) {
+        const uint2 q = ok ? static_cast<const uint2 *>(rmask_v)[L] : make_uint2(0u, 0u);
+        mw[0][g] = q.x, mw[1][g] = q.y;
+      } else {
+        mw[0][g] = ok ? static_cast<const uint32_t *>(rmask_v)[L] : 0u;
+      }
       info[g] = ok ? rowinfo[L] : kRowHole;
       rold[g] = ok ? r[L] : 0.0;
       S[g] = 0.0;
@@ -660,8 +669,13 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
         const int s = __builtin_amdgcn_readlane(cs, y), e = __builtin_amdgcn_readlane(ce, y);
         if (e == s) continue;
         const int sa = s & ~1;
-        if (C <= 32 || y < 32) epi_class_add<G>(mlo, 1u << (y & 31), fill + (s - sa), win, W, S);
-        else epi_class_add<G>(mhi, 1u << (y & 31), fill + (s - sa), win, W, S);
+        const uint32_t bit = 1u << (y & 31);
+        const int run = fill + (s - sa);
+        // static word index (a runtime index into mw would put it in scratch)
+        if (MW == 1 || y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
+        else if (MW == 2 || y < 64) epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
+        else if (y < 96) epi_class_add<G>(mw[MW > 2 ? 2 : 0], bit, run, win, W, S);
+        else epi_class_add<G>(mw[MW > 3 ? 3 : 0], bit, run, win, W, S);
         fill += ((e + 1) & ~1) - sa;
       }
       __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
@@ -671,7 +685,10 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     for (int g = 0; g < G; ++g) {
       const int64_t L = (b0 + g) * kWave + lane;
       double Sv = S[g];
-      if ((mlo[g] | mhi[g]) == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
+      uint32_t any = 0u;
+#pragma unroll
+      for (int w = 0; w < MW; ++w) any |= mw[w][g];
+      if (any == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
       const double rn = affine(Sv, tdc, teleport, damping);
       if (!(info[g] & kRowHole)) {
         r[L] = rn;
@@ -702,6 +719,7 @@ inline EpiGrpFn epi_grp_kernel_c(int var) {
   }
 }
 inline EpiGrpFn epi_grp_kernel(int C, int var) {
+  if (C == 128) return epi_grp_kernel_c<128>(var);
   return C == 64 ? epi_grp_kernel_c<64>(var)
                  : (C == 32 ? epi_grp_kernel_c<32>(var) : (C == 16 ? epi_grp_kernel_c<16>(var) : epi_grp_kernel_c<8>(var)));
 }

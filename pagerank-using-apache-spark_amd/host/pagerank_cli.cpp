@@ -2,6 +2,7 @@
 //
 //   pagerank <input-path> [iterations=10] [--format=edges|ccjson] [--out DIR]
 //            [--save-every-iter] [--dangling=local|none] [--device N] [--quiet] [--stats]
+//            [--resume DIR/PageRank<i>]
 //
 // Input (libpagerank_host): "src dst" edge list ("src" alone = record without links), or
 // --format=ccjson "url<TAB>json" Common Crawl metadata records (Sparky.java:61-123).  URLs are
@@ -10,6 +11,10 @@
 // Output: "Starting iter<i>" before each iteration (Sparky.java:188), then one
 // "<url> has rank: <r>." line per URL (north_star); --out DIR writes DIR/PageRank<i>/part-00000
 // "(url,rank)" + _SUCCESS (Sparky.java:237) for the last (or every) iteration.
+// --resume DIR/PageRank<i>: start from the ranks a previous run (or Sparky.java:237) saved there
+// instead of 1.0 (Sparky.java:165-170) and continue the same loop: iterations i+1 .. N-1, with
+// the same "Starting iter" lines and PageRank<iter> numbering.  A directory not named
+// PageRank<i> starts the loop at 0.
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -21,7 +26,7 @@
 namespace {
 
 struct Options {
-  std::string path, out;
+  std::string path, out, resume;
   int iterations = 10;  // Sparky.java:187
   int format = PRH_FORMAT_EDGES;
   bool save_every = false, quiet = false, stats = false;
@@ -33,7 +38,8 @@ struct Options {
   if (msg) std::fprintf(stderr, "pagerank: %s\n", msg);
   std::fprintf(stderr,
                "usage: pagerank <input-path> [iterations=10] [--format=edges|ccjson] [--out DIR]\n"
-               "                [--save-every-iter] [--dangling=local|none] [--device N] [--quiet] [--stats]\n");
+               "                [--save-every-iter] [--dangling=local|none] [--device N] [--quiet] [--stats]\n"
+               "                [--resume DIR/PageRank<i>]\n");
   std::exit(2);
 }
 
@@ -52,6 +58,8 @@ Options parse(int argc, char **argv) {
     else if (a == "--dangling=local") o.flags = PR_DANGLING_LOCAL;
     else if (a == "--dangling=none") o.flags = PR_DANGLING_NONE;
     else if (a == "--device" && i + 1 < argc) o.device = std::atoi(argv[++i]);
+    else if (a == "--resume" && i + 1 < argc) o.resume = argv[++i];
+    else if (a.rfind("--resume=", 0) == 0) o.resume = a.substr(9);
     else if (a == "-h" || a == "--help") usage(nullptr);
     else if (!a.empty() && a[0] == '-') usage(("unknown option " + a).c_str());
     else if (pos == 0) { o.path = a; ++pos; }
@@ -66,12 +74,25 @@ Options parse(int argc, char **argv) {
 struct Job {
   const Options *opt;
   const prh_edges *edges;
+  int start = 0;  // global index of the run's first iteration (--resume)
   int error = 0;
 };
 
-void on_iter(int32_t it, const double *ranks, double dc, double l1, double ms, void *user) {
+// i of a ".../PageRank<i>" directory (trailing '/' allowed), or -1
+int saved_iteration(std::string d) {
+  while (d.size() > 1 && d.back() == '/') d.pop_back();
+  const size_t slash = d.rfind('/');
+  const std::string base = slash == std::string::npos ? d : d.substr(slash + 1);
+  if (base.rfind("PageRank", 0) != 0 || base.size() == 8) return -1;
+  for (size_t k = 8; k < base.size(); ++k)
+    if (base[k] < '0' || base[k] > '9') return -1;
+  return std::atoi(base.c_str() + 8);
+}
+
+void on_iter(int32_t it_run, const double *ranks, double dc, double l1, double ms, void *user) {
   Job *job = static_cast<Job *>(user);
   const Options &o = *job->opt;
+  const int32_t it = job->start + it_run;
   if (!o.out.empty() && ranks && (o.save_every || it == o.iterations - 1)) {
     if (prh_write_part(job->edges, o.out.c_str(), it, ranks) != 0) {
       std::fprintf(stderr, "pagerank: %s\n", prh_last_error());
@@ -102,9 +123,20 @@ int main(int argc, char **argv) {
     return 1;
   }
   Job job{&o, edges};
-  std::vector<double> ranks((size_t)V + 1);
-  if (o.iterations > 0) std::printf("Starting iter0\n");
-  rc = pr_run(g, o.iterations, 0.15, 0.85, nullptr, ranks.data(), on_iter,
+  std::vector<double> ranks((size_t)V + 1), init;
+  if (!o.resume.empty()) {
+    init.assign((size_t)V + 1, 0.0);
+    if (prh_read_ranks(edges, o.resume.c_str(), init.data()) != 0) {
+      std::fprintf(stderr, "pagerank: --resume: %s\n", prh_last_error());
+      pr_graph_destroy(g);
+      prh_free(edges);
+      return 1;
+    }
+    job.start = saved_iteration(o.resume) + 1;  // 0 when the directory is not PageRank<i>
+  }
+  const int n_run = o.iterations > job.start ? o.iterations - job.start : 0;
+  if (n_run > 0) std::printf("Starting iter%d\n", job.start);
+  rc = pr_run(g, n_run, 0.15, 0.85, init.empty() ? nullptr : init.data(), ranks.data(), on_iter,
               o.out.empty() ? 0u : PR_CB_RANKS, &job);
   pr_graph_destroy(g);
   if (rc != PR_OK) {

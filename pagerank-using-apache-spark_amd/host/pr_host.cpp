@@ -7,14 +7,20 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <dirent.h>
+
+#include <algorithm>
 #include <cerrno>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <memory>
 #include <string>
 #include <string_view>
+#include <unordered_map>
 #include <utility>
 #include <vector>
 
@@ -553,6 +559,66 @@ int prh_write_has_rank(const prh_edges *e, const char *path, const double *ranks
   if (path) std::fclose(f);
   else std::fflush(f);
   return rc;
+}
+
+// Resume: the "(url,rank)" lines of every part-* file of a saveAsTextFile
+// directory (Sparky.java:237), mapped through the interned names.  Every URL of the edge list
+// must appear exactly once and no other URL may; the rank is the text Double.toString wrote
+// (shortest round-trip digits), so strtod restores the saved double exactly.
+int prh_read_ranks(const prh_edges *e, const char *dir, double *ranks) {
+  if (!e || !dir || !ranks) return fail("NULL argument");
+  DIR *d = opendir(dir);
+  if (!d) return fail(std::string("cannot open directory ") + dir + ": " + std::strerror(errno));
+  std::vector<std::string> parts;
+  while (struct dirent *de = readdir(d)) {
+    const std::string n = de->d_name;
+    if (n.rfind("part-", 0) == 0) parts.push_back(n);
+  }
+  closedir(d);
+  if (parts.empty()) return fail(std::string("no part-* files in ") + dir);
+  std::sort(parts.begin(), parts.end());
+  std::unordered_map<std::string_view, int32_t> id;
+  id.reserve(e->names.size() * 2);
+  for (size_t v = 0; v < e->names.size(); ++v) id.emplace(e->names[v], (int32_t)v);
+  std::vector<uint8_t> seen(e->names.size(), 0);
+  size_t n_seen = 0;
+  for (const std::string &pn : parts) {
+    const std::string path = std::string(dir) + "/" + pn;
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) return fail("cannot open " + path);
+    std::string data;
+    char buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof(buf), f)) > 0) data.append(buf, k);
+    std::fclose(f);
+    size_t i = 0, lineno = 0;
+    while (i < data.size()) {
+      ++lineno;
+      size_t b = i;
+      while (i < data.size() && data[i] != '\n') ++i;
+      size_t t = i++;
+      if (t > b && data[t - 1] == '\r') --t;
+      if (t == b) continue;
+      const std::string where = path + ":" + std::to_string(lineno);
+      if (data[b] != '(' || data[t - 1] != ')') return fail(where + ": expected '(url,rank)'");
+      const std::string_view body(data.data() + b + 1, t - b - 2);
+      const size_t c = body.rfind(',');  // URLs may hold commas; the rank never does
+      if (c == std::string_view::npos) return fail(where + ": expected '(url,rank)'");
+      const std::string num(body.substr(c + 1));
+      char *endp = nullptr;
+      const double r = std::strtod(num.c_str(), &endp);
+      if (num.empty() || *endp != '\0') return fail(where + ": bad rank '" + num + "'");
+      auto it = id.find(body.substr(0, c));
+      if (it == id.end()) return fail(where + ": URL not in the edge list");
+      if (seen[it->second]) return fail(where + ": URL listed twice");
+      seen[it->second] = 1;
+      ++n_seen;
+      ranks[it->second] = r;
+    }
+  }
+  if (n_seen != e->names.size())
+    return fail(std::string(dir) + ": " + std::to_string(e->names.size() - n_seen) + " URL(s) of the edge list have no saved rank");
+  return 0;
 }
 
 void prh_free(prh_edges *e) { delete e; }

@@ -46,6 +46,7 @@ def load() -> ctypes.CDLL:
         L.prh_java_double.restype = ctypes.c_int32
         L.prh_write_part.argtypes = [P, ctypes.c_char_p, ctypes.c_int32, P]
         L.prh_write_has_rank.argtypes = [P, ctypes.c_char_p, P]
+        L.prh_read_ranks.argtypes = [P, ctypes.c_char_p, P]
         L.prh_free.argtypes = [P]
         L.prh_free.restype = None
         _hl = L
@@ -100,6 +101,12 @@ class HostEdges:
         r = np.ascontiguousarray(ranks, dtype=np.float64)
         _check(load().prh_write_has_rank(self._h, path.encode() if path else None,
                                          r.ctypes.data_as(ctypes.c_void_p)))
+
+    def read_ranks(self, directory: str) -> np.ndarray:
+        """Resume input: the saved ``(url,rank)`` lines of ``directory/part-*`` in ID order."""
+        r = np.zeros(max(self.n_vertices, 1), np.float64)
+        _check(load().prh_read_ranks(self._h, directory.encode(), r.ctypes.data_as(ctypes.c_void_p)))
+        return r[: self.n_vertices]
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

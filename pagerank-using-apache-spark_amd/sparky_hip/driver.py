@@ -1,7 +1,8 @@
 """Process-level drop-in for the Spark job (Python host; the C++ CLI ``pagerank`` is the same).
 
 CLI: ``python -m sparky_hip <input-path> [iterations=10] [--format edges|ccjson]
-[--out DIR] [--save-every-iter] [--dangling=local|none] [--device N] [--quiet]``
+[--out DIR] [--save-every-iter] [--dangling=local|none] [--device N] [--quiet]
+[--resume DIR/PageRank<i>]``
 
 * input: text edge list, ``src dst`` per line; a single-token line ``src`` is a record without
   ``a`` links (Sparky.java:114-118).  Tokens (URLs) are taken verbatim and interned to dense
@@ -12,6 +13,9 @@ CLI: ``python -m sparky_hip <input-path> [iterations=10] [--form
   ``Tuple2.toString`` of ``(String, Double)`` with Java ``Double.toString`` -- plus an empty
   ``_SUCCESS`` (Sparky.java:237 ``saveAsTextFile``); only the last iteration unless
   ``--save-every-iter``.
+* ``--resume DIR/PageRank<i>``: start from the ranks saved there (instead of 1.0,
+  Sparky.java:165-170) and continue the same loop with iterations i+1 .. N-1 (a directory not
+  named ``PageRank<i>`` starts the loop at 0).  Same rules as the C++ CLI.
 """
 from __future__ import annotations
 
@@ -121,6 +125,14 @@ def write_has_rank(stream: TextIO, urls: Sequence[str], ranks: np.ndarray) -> No
         stream.write(f"{u} has rank: {java_double_to_string(r)}.\n")
 
 
+def saved_iteration(path: str) -> int:
+    """i of a ``.../PageRank<i>`` directory, or -1."""
+    base = os.path.basename(os.path.normpath(path))
+    if base.startswith("PageRank") and base[8:].isdigit():
+        return int(base[8:])
+    return -1
+
+
 def main(argv=None) -> int:
     from ._host import HostEdges
 
@@ -133,22 +145,29 @@ def main(argv=None) -> int:
     ap.add_argument("--dangling", choices=["local", "none"], default="local")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--quiet", action="store_true", help="omit the '<url> has rank' lines")
+    ap.add_argument("--resume", default=None, metavar="DIR", help="start from saved (url,rank) part files")
     a = ap.parse_args(argv)
     edges = HostEdges.read(a.edge_list, a.format)  # native front-end + first-appearance interning
     out = sys.stdout
+    init, start = None, 0
+    if a.resume:
+        init = edges.read_ranks(a.resume)
+        start = saved_iteration(a.resume) + 1
+    n_run = max(a.iterations - start, 0)
     with PageRankGraph(edges.n_vertices, edges.src, edges.dst, device=a.device, dangling=a.dangling,
                        keep_canonical=False) as g:
         # Sparky prints "Starting iter<i>" before each iteration (Sparky.java:188); the library
         # calls back after iteration i, so the host prints the next line there.
-        def cb(it, ranks, _st):
+        def cb(it_run, ranks, _st):
+            it = start + it_run
             if a.out and (a.save_every_iter or it == a.iterations - 1):
                 edges.write_part(a.out, it, ranks)
             if it + 1 < a.iterations:
                 out.write(f"Starting iter{it + 1}\n")
 
-        if a.iterations > 0:
-            out.write("Starting iter0\n")
-        ranks, _ = g.run(a.iterations, callback=cb, want_ranks_in_callback=bool(a.out))
+        if n_run > 0:
+            out.write(f"Starting iter{start}\n")
+        ranks, _ = g.run(n_run, callback=cb, want_ranks_in_callback=bool(a.out), init_ranks=init)
     out.flush()
     if not a.quiet:
         edges.write_has_rank(None, ranks)

@@ -41,6 +41,16 @@ class IterationStats:
     ms: float
 
 
+def _init_array(init_ranks, n_vertices: int):
+    """init_ranks as a contiguous float64[V] (the C side reads exactly V doubles), or None."""
+    if init_ranks is None:
+        return None
+    init = np.ascontiguousarray(init_ranks, dtype=np.float64)
+    if init.shape != (n_vertices,):
+        raise ValueError(f"init_ranks must have shape ({n_vertices},), got {init.shape}")
+    return init
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     check(_lib.load().pr_device_count(ctypes.byref(n)))
@@ -140,24 +150,32 @@ class PageRankGraph:
         per-iteration stats.  ``callback(iter, ranks_or_None, stats)`` runs between iterations."""
         V = self.n_vertices
         out = np.zeros(max(V, 1), np.float64)
-        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        init = _init_array(init_ranks, V)
         history: List[IterationStats] = []
+        errors: List[BaseException] = []
 
         def _cb(it, rp, dc, l1, ms, _user):
+            # ctypes only prints an exception raised in a callback; keep the first one and
+            # re-raise it once pr_run returns (later iterations skip the user callback)
             st = IterationStats(int(it), float(dc), float(l1), float(ms))
             history.append(st)
-            if callback is not None:
-                arr = np.ctypeslib.as_array(rp, shape=(V,)).copy() if rp else None
-                callback(int(it), arr, st)
+            if callback is not None and not errors:
+                try:
+                    arr = np.ctypeslib.as_array(rp, shape=(V,)).copy() if rp else None
+                    callback(int(it), arr, st)
+                except BaseException as e:  # noqa: B902 -- re-raised below
+                    errors.append(e)
 
         cb = _lib.ITER_CB(_cb)
         flags = _lib.PR_CB_RANKS if want_ranks_in_callback else 0
         check(_lib.load().pr_run(self._h, int(iterations), teleport, damping, _ptr(init), _ptr(out),
                                  cb, flags, None))
+        if errors:
+            raise errors[0]
         return out[:V], history
 
     def reset(self, *, teleport: float = 0.15, damping: float = 0.85, init_ranks=None) -> None:
-        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        init = _init_array(init_ranks, self.n_vertices)
         check(_lib.load().pr_reset(self._h, teleport, damping, _ptr(init)))
 
     def step(self, iterations: int) -> None:
@@ -233,7 +251,7 @@ class PartGroup:
         self._arr = (ctypes.c_void_p * n)(*[p._h.value for p in self.parts])
 
     def reset(self, *, teleport=0.15, damping=0.85, init_ranks=None):
-        init = None if init_ranks is None else np.ascontiguousarray(init_ranks, dtype=np.float64)
+        init = _init_array(init_ranks, self.parts[0].n_vertices)
         check(_lib.load().pr_group_reset(self._arr, len(self.parts), teleport, damping, _ptr(init)))
 
     def step(self, iterations: int):

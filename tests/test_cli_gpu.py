@@ -89,3 +89,56 @@ def test_cli_rejects_bad_input(tmp_path):
     inp.write_text("a b c\n")
     res = subprocess.run([CLI, str(inp)], capture_output=True, text=True, timeout=60)
     assert res.returncode != 0 and "tokens" in res.stderr
+
+
+@pytest.mark.parametrize("runner", ["cpp", "python"])
+def test_cli_resume_from_saved_iteration(tmp_path, runner, oracle_c):
+    """--resume DIR/PageRank4 continues the same 10-iteration loop (iterations 5..9): the saved
+    Double.toString digits restore the ranks exactly, so PageRank9 matches the uninterrupted run
+    (to rounding: the resumed dc is summed by k_reset's blocks, not the epilogue's) and the
+    continued ranks match the oracle started from the saved ranks (oracle_c.run(..., init=...)).
+    Reference: Sparky.java:165-170 (init) and :237 (the saves)."""
+    rng = np.random.default_rng(12)
+    lines = [f"u{int(s)} u{int(d)}" for s, d in zip(rng.integers(0, 400, 3000), rng.integers(0, 500, 3000))]
+    lines += [f"u{i}" for i in range(400, 420)]  # records without links
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(lines) + "\n")
+    env = dict(os.environ, PYTHONPATH=PKG_DIR)
+    base = [CLI] if runner == "cpp" else [sys.executable, "-m", "sparky_hip"]
+    full, part = tmp_path / "full", tmp_path / "cont"
+    r1 = subprocess.run(base + [str(inp), "10", "--out", str(full), "--save-every-iter", "--quiet"],
+                        capture_output=True, text=True, env=env, timeout=120)
+    assert r1.returncode == 0, r1.stderr
+    r2 = subprocess.run(base + [str(inp), "10", "--out", str(part), "--save-every-iter", "--quiet",
+                                "--resume", str(full / "PageRank4")], capture_output=True, text=True, env=env,
+                        timeout=120)
+    assert r2.returncode == 0, r2.stderr
+    assert r2.stdout.splitlines() == [f"Starting iter{i}" for i in range(5, 10)]
+    assert not (part / "PageRank4").exists() and (part / "PageRank5" / "_SUCCESS").exists()
+    a9, b9 = parse_part(part / "PageRank9" / "part-00000"), parse_part(full / "PageRank9" / "part-00000")
+    assert a9.keys() == b9.keys() and max(abs(a9[u] - b9[u]) / b9[u] for u in a9) <= 1e-13
+    # oracle: 5 iterations from the saved PageRank4 ranks
+    from sparky_hip import read_edge_list
+
+    urls, src, dst = read_edge_list(lines)
+    saved = parse_part(full / "PageRank4" / "part-00000")
+    init = np.array([saved[u] for u in urls])
+    ref = oracle_c.run(oracle_c.build_csr(len(urls), src, dst), 5, init=init)
+    got = parse_part(part / "PageRank9" / "part-00000")
+    err = max(abs(got[u] - ref["ranks"][i]) / ref["ranks"][i] for i, u in enumerate(urls))
+    assert err <= 1e-9
+
+
+@pytest.mark.parametrize("runner", ["cpp", "python"])
+def test_cli_unwritable_out_fails(tmp_path, runner):
+    """A failed saveAsTextFile (here: --out below a regular file) must end the job with a non-zero
+    status, from the C++ CLI and from the Python host (whose writer runs inside a ctypes callback)."""
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(KAT) + "\n")
+    blocker = tmp_path / "file"
+    blocker.write_text("x")
+    env = dict(os.environ, PYTHONPATH=PKG_DIR)
+    base = [CLI] if runner == "cpp" else [sys.executable, "-m", "sparky_hip"]
+    res = subprocess.run(base + [str(inp), "3", "--out", str(blocker / "out")], capture_output=True, text=True,
+                         env=env, timeout=120)
+    assert res.returncode != 0

@@ -291,14 +291,18 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
                                                              (32, "1", "1", "0"), (32, "1", "1", "1"),
                                                              (32, "1", "1", "v1"), (32, "1", "1", "v2"),
                                                              (32, "1", "1", "v4"), (64, "0", "1", "1"),
-                                                             (64, "1", "1", "1"), (64, "1", "1", "v2")])
+                                                             (64, "1", "1", "1"), (64, "1", "1", "v2"),
+                                                             (64, "1", "0", "1"), (128, "0", "1", "1"),
+                                                             (128, "1", "1", "1"), (128, "1", "0", "v2")])
 def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp, monkeypatch):
     """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
     after another with the hot set restaged per class) and the three epilogues: grouped (class
     runs of 8 blocks staged in LDS; here ~10 segments per row, so a group's runs take several
     window loads), one load per class and block over all partials, or one buffer per class (the
     > 2^29-slot path, which also turns the grouped one off); the grouped one in several (blocks
-    per group, LDS window) variants.  Default: 32 classes, phased, grouped."""
+    per group, LDS window) variants.  (64, PR_EPI_ABS=0): the grouped epilogue without the
+    < 2^29-slot byte-offset path, as a graph with more than 2^29 partial slots builds it.  128
+    classes: four mask words per row.  Default policy: up to 64 classes, phased, grouped."""
     monkeypatch.setenv("PR_CLASSES", str(classes))
     monkeypatch.setenv("PR_HOT_PHASED", phased)
     monkeypatch.setenv("PR_EPI_ABS", epi_abs)

@@ -83,3 +83,73 @@ def test_cpp_formatter_matches_python():
     out = subprocess.run([exe], input=inp, capture_output=True, text=True, check=True).stdout.split("\n")
     for v, s in zip(vals, out):
         assert s == java_double_to_string(v), (v, s)
+
+
+# ---- resume input: saved (url,rank) part files back to ranks in ID order ----
+def _edges(lines):
+    from sparky_hip._host import HostEdges
+
+    return HostEdges.parse("\n".join(lines).encode())
+
+
+def test_read_ranks_round_trips_saved_part_files_exactly(tmp_path):
+    rng = random.Random(3)
+    lines = [f"http://s{i}.org/a,b?x={i} http://s{(i * 7) % 60}.org/" for i in range(60)] + ["lonely"]
+    e = _edges(lines)
+    ranks = np.array([rng.uniform(0.15, 40.0) for _ in range(e.n_vertices)])
+    ranks[3] = 1e-5  # exponent form "1.0E-5"
+    e.write_part(str(tmp_path), 4, ranks)
+    got = e.read_ranks(str(tmp_path / "PageRank4"))
+    assert np.array_equal(got, ranks)  # Double.toString digits restore the double exactly
+    e.close()
+
+
+def test_read_ranks_reads_every_part_file_and_any_line_order(tmp_path):
+    e = _edges(["a b", "b c", "c a"])
+    d = tmp_path / "PageRank0"
+    d.mkdir()
+    (d / "part-00000").write_text("(c,0.5)\n")
+    (d / "part-00001").write_text("(b,2.0E-3)\r\n\n(a,1.25)\n")
+    (d / "_SUCCESS").write_text("")
+    assert e.read_ranks(str(d)).tolist() == [1.25, 0.002, 0.5]
+    e.close()
+
+
+@pytest.mark.parametrize("content,msg", [
+    ("(a,1.0)\n(b,1.0)\n", "no saved rank"),              # c missing
+    ("(a,1.0)\n(b,1.0)\n(c,1.0)\n(zz,1.0)\n", "not in the edge list"),
+    ("(a,1.0)\n(a,1.0)\n(b,1.0)\n(c,1.0)\n", "twice"),
+    ("a,1.0\n", "expected"),
+    ("(a,one)\n", "bad rank"),
+])
+def test_read_ranks_rejects_inconsistent_saves(tmp_path, content, msg):
+    from sparky_hip._host import HostError
+
+    e = _edges(["a b", "b c", "c a"])
+    d = tmp_path / "PageRank1"
+    d.mkdir()
+    (d / "part-00000").write_text(content)
+    with pytest.raises(HostError) as ei:
+        e.read_ranks(str(d))
+    assert msg in str(ei.value)
+    with pytest.raises(HostError):
+        e.read_ranks(str(tmp_path / "missing"))
+    e.close()
+
+
+def test_saved_iteration_numbering():
+    from sparky_hip.driver import saved_iteration
+
+    assert saved_iteration("/x/out/PageRank4") == 4
+    assert saved_iteration("/x/out/PageRank12/") == 12
+    assert saved_iteration("/x/out/PageRank") == -1
+    assert saved_iteration("/x/out/ranks") == -1
+
+
+def test_init_ranks_length_is_checked():
+    from sparky_hip.graph import _init_array
+
+    assert _init_array(None, 3) is None
+    assert _init_array([1, 2, 3], 3).dtype == np.float64
+    with pytest.raises(ValueError):
+        _init_array(np.ones(2), 3)
