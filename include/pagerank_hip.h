@@ -129,7 +129,9 @@ int pr_run(pr_graph *g, int32_t iterations, double teleport, double damping,
            void *user);
 
 /* Lower-level stepping (resume from saved ranks, benchmarking).  pr_step enqueues work on
- * the library's stream and returns; pr_sync waits for it. */
+ * the library's stream and returns; pr_sync waits for it.  init_ranks (pr_run, pr_reset,
+ * pr_group_reset): NULL (every rank 1.0, Sparky.java:165-170) or V doubles in original-ID
+ * order; the library reads exactly V of them. */
 int pr_reset(pr_graph *g, double teleport, double damping, const double *init_ranks);
 int pr_step(pr_graph *g, int32_t iterations);
 int pr_sync(pr_graph *g);
@@ -138,8 +140,10 @@ int pr_set_timing(pr_graph *g, int32_t enable);
 int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes
- * to every rank (any channel), every rank attaches it to its part.  Parts exchange the
- * contribution vector with an RCCL all-gather over xGMI once per iteration. */
+ * to every rank (any channel), every rank attaches it to its part.  Once per iteration each
+ * part sends every peer exactly the contributions (and the two dangling/L1 slots) that the
+ * peer's in-links read, with grouped RCCL ncclSend/ncclRecv over xGMI (PR_EXCHANGE=allgather:
+ * one ncclAllGather of whole slices instead).  Attach cross-checks the per-peer run lengths. */
 #define PR_COMM_ID_BYTES 128
 int pr_comm_unique_id(uint8_t *id_out);
 int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8_t *id);

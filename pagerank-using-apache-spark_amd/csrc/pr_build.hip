@@ -15,6 +15,7 @@
 #include "pr_compact.h"
 #include "pr_device.h"
 #include "pr_graph.h"
+#include "pr_plan.h"
 
 namespace pr {
 namespace {
@@ -174,17 +175,6 @@ __global__ void k_row_ptr_seg(const uint64_t *__restrict__ keys, int64_t lo, int
   }
 }
 
-// Class boundaries of the sorted local keys: cls_start[x] = first key of class >= x.
-__global__ void k_class_bounds(const uint64_t *__restrict__ keys, int64_t m, int shift, int C,
-                               int64_t *__restrict__ cls_start) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= m;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t xc = (i < m) ? (int64_t)(keys[i] >> shift) : C;
-    const int64_t xp = (i > 0) ? (int64_t)(keys[i - 1] >> shift) : -1;
-    for (int64_t x = xp + 1; x <= xc; ++x) cls_start[x] = i;
-  }
-}
-
 __global__ void k_local_col(const uint64_t *__restrict__ keys, int64_t m, uint64_t mask,
                             int32_t *__restrict__ col) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m;
@@ -293,66 +283,7 @@ int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, h
   return PR_OK;
 }
 
-// ---- split layout: wave units + entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) -----------
-struct WavePlan {
-  std::vector<Unit> units;       // p8 = entry offset / 8, r0 = first slot, meta, n = padded entries
-  std::vector<int64_t> src_off;  // first in-link of the unit in the part's column array
-  std::vector<int32_t> n_real;   // in-links of the unit (without padding)
-  std::vector<int64_t> ucum;     // units of class < x
-  int64_t len = 0;               // entries (padded)
-};
-
-// Class x of one part: segments = rows with at least one class-x in-link, in row order; segment
-// k has slot k (its partial sum lands in part_x[k]).  Greedy, linear, deterministic: consecutive
-// segments while they fit kWaveUnit entries; a longer segment becomes PIECE units.  Also records
-// base[blk][x] (stride C) = slot of the first segment at or after row 64*blk (the epilogue's
-// slot lookup).
-static void plan_class_units(const std::vector<int64_t> &rp, int64_t lo, int x, int C, WavePlan *wp, int64_t *pieces,
-                             std::vector<int32_t> *seg_cls, std::vector<int64_t> *seg_slot,
-                             std::vector<int32_t> *seg_p0, int32_t *base, int64_t *n_slots) {
-  const int64_t R = (int64_t)rp.size() - 1, cap = kWaveUnit;
-  auto push = [&](int64_t src, int64_t r0, int64_t meta, int64_t n) {
-    const int64_t np = (n + kWavePT - 1) / kWavePT * kWavePT;
-    wp->units.push_back(Unit{(uint32_t)(wp->len / 8), (int32_t)r0, (int32_t)meta, (int32_t)np});
-    wp->src_off.push_back(lo + src);
-    wp->n_real.push_back((int32_t)n);
-    wp->len += np;
-  };
-  int64_t slot = 0, u_r0 = 0, u_src = 0, u_n = 0, u_seg = 0;
-  auto flush = [&]() {
-    if (u_seg > 0) push(u_src, u_r0, u_seg, u_n);
-    u_seg = 0;
-    u_n = 0;
-  };
-  for (int64_t L = 0; L < R; ++L) {
-    if ((L & 63) == 0) base[(L >> 6) * C] = (int32_t)slot;
-    const int64_t len = rp[L + 1] - rp[L];
-    if (len == 0) continue;
-    if (len > cap) {
-      flush();
-      const int64_t np = (len + cap - 1) / cap;
-      seg_cls->push_back(x);
-      seg_slot->push_back(slot);
-      seg_p0->push_back((int32_t)*pieces);
-      for (int64_t q = 0; q < np; ++q)
-        push(rp[L] + q * cap, slot, -(*pieces + q) - 1, std::min<int64_t>(cap, len - q * cap));
-      *pieces += np;
-      ++slot;
-      continue;
-    }
-    if (u_seg > 0 && u_n + len > cap) flush();
-    if (u_seg == 0) {
-      u_r0 = slot;
-      u_src = rp[L];
-    }
-    u_n += len;
-    ++u_seg;
-    ++slot;
-  }
-  flush();
-  *n_slots = slot;
-}
-
+// ---- split layout: entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) -----------------------
 // Entry code (pr_internal.h); a segment end is marked in bit 0 until k_unit_meta moves it into
 // the lane metadata (codes are byte offsets / addresses, multiples of 8).
 // hpos[x * P*Kp + p*Kp + q] = gather position of row x*Q_pad + q of part p (0 when q >= q_load or
@@ -387,29 +318,6 @@ __global__ void k_map_cols(int64_t n, const int32_t *__restrict__ cmap, int32_t 
     const int32_t c = cmap[col[i]];
     if (c < 0) atomicAdd(bad, 1ull);
     col[i] = c < 0 ? 0 : c;
-  }
-}
-
-// Marks the last in-link of every non-empty row of a class CSR (bit 31 of the column entry;
-// gather positions are < 2^28 in the split layout).
-__global__ void k_mark_ends(int64_t R, const int64_t *__restrict__ rp, int32_t *__restrict__ col) {
-  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = rp[L + 1];
-    if (e > rp[L]) col[e - 1] |= (int32_t)0x80000000u;
-  }
-}
-
-// Row class masks: bit x when the row has a class-x in-link (nw 32-bit words per row).
-__global__ void k_row_masks(int64_t R, int C, int nw, const int64_t *__restrict__ rp_all, uint32_t *__restrict__ rmask) {
-  for (int64_t L = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; L < R; L += (int64_t)gridDim.x * blockDim.x) {
-    for (int w = 0; w < nw; ++w) {
-      uint32_t m = 0;
-      for (int b = 0; b < 32 && 32 * w + b < C; ++b) {
-        const int64_t *rp = rp_all + (int64_t)(32 * w + b) * (R + 1);
-        if (rp[L + 1] > rp[L]) m |= 1u << b;
-      }
-      rmask[L * nw + w] = m;
-    }
   }
 }
 
@@ -658,13 +566,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipStreamSynchronize(s));
     if (hb) return fail(PR_ERR_STATE, "exchange lists miss a source of this part's in-links");
   }
-  DevBuf cls_start;
-  PR_TRY(cls_start.alloc(sizeof(int64_t) * (C + 1)));
-  hipLaunchKernelGGL(k_class_bounds, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s,
-                     keys.as<uint64_t>(), lm, bg + brow, C, cls_start.as<int64_t>());
-  std::vector<int64_t> hcls(C + 1);
-  PR_HIP(hipMemcpyAsync(hcls.data(), cls_start.p, sizeof(int64_t) * (C + 1), hipMemcpyDeviceToHost, s));
-  PR_HIP(hipStreamSynchronize(s));
   PR_TRY(g->rowinfo.alloc(sizeof(uint32_t) * ((size_t)R + 1)));
   DevBuf orig;
   PR_TRY(orig.alloc(sizeof(int32_t) * ((size_t)R + 1)));
@@ -677,17 +578,14 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   rank_of.reset();
   gpos.reset();
 
-  // ---- work plans (host greedy) ----
+  // ---- work plans (fused: host greedy over the row pointers; split: pr_plan.hip on the GPU) ----
   const uint64_t rmask = (uint64_t(1) << brow) - 1;
   std::vector<int64_t> rp;
-  std::vector<int32_t> seg_cls, seg_p0;
-  std::vector<int64_t> seg_slot;
+  std::vector<int32_t> seg_p0;
   std::vector<int32_t> lr_row, lr_p0;
   std::vector<Unit> light_units;
   int64_t pieces = 0;
-  WavePlan wp;
   g->nblk = (R + 63) / 64;
-  std::vector<int32_t> hbase;
   std::vector<int64_t> poff(kMaxClasses + 1, 0);
   if (C == 1) {
     // fused layout: one CSR over all rows, 256-thread units with the fused epilogue
@@ -713,29 +611,16 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(build_padded_cols(px, g->col.as<int32_t>(), g->colp.as<int32_t>(), s));
     seg_p0.push_back(0);
   } else {
-    // split layout: per class, the segments of the rows with class-x in-links -> wave units
-    DevBuf rp_all;
-    PR_TRY(rp_all.alloc(sizeof(int64_t) * (size_t)C * (R + 1)));
-    hbase.assign((size_t)C * g->nblk, 0);
-    for (int x = 0; x < C; ++x) {
-      int64_t *rpd = rp_all.as<int64_t>() + (size_t)x * (R + 1);
-      hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(hcls[x + 1] - hcls[x] + 1, T, 65536)), dim3(T), 0, s,
-                         keys.as<uint64_t>(), hcls[x], hcls[x + 1], bg, rmask, R, rpd);
-      hipLaunchKernelGGL(k_mark_ends, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, rpd,
-                         g->col.as<int32_t>() + hcls[x]);
-      PR_HIP(hipGetLastError());
-      rp.assign((size_t)R + 1, 0);
-      PR_HIP(hipMemcpyAsync(rp.data(), rpd, sizeof(int64_t) * rp.size(), hipMemcpyDeviceToHost, s));
-      PR_HIP(hipStreamSynchronize(s));
-      wp.ucum.push_back((int64_t)wp.units.size());
-      int64_t n_slots = 0;
-      plan_class_units(rp, hcls[x], x, C, &wp, &pieces, &seg_cls, &seg_slot, &seg_p0, hbase.data() + x, &n_slots);
-      poff[x + 1] = poff[x] + n_slots;
-      if (n_slots >= (int64_t(1) << 29)) return fail(PR_ERR_INVALID, "a column class exceeds 2^29 segments");
-    }
+    // split layout: segments (row, class), class masks, block bases and wave units, planned on
+    // the GPU (pr_plan.hip); the slot of segment k is k, so the class boundaries are poff
+    SplitPlanner sp;
+    PR_TRY(sp.segments(keys.as<uint64_t>(), lm, bg, brow, C, R, g->col.as<int32_t>(), s));
     keys.reset();
     tmp.reset();
+    for (int x = 0; x <= C; ++x) poff[x] = sp.cseg[x];
     for (int x = C; x < kMaxClasses; ++x) poff[x + 1] = poff[x];
+    for (int x = 0; x < C; ++x)
+      if (poff[x + 1] - poff[x] >= (int64_t(1) << 29)) return fail(PR_ERR_INVALID, "a column class exceeds 2^29 segments");
     // k_epilogue<C, true>: one buffer resource over all partials, so every partial needs a 32-bit
     // byte offset (< 2^29 slots).  k_epilogue_grp addresses partials through int32 absolute slot
     // indices (< 2^31 slots: R-MAT s26 has ~2^28.1, a graph 7x its size still fits).
@@ -746,26 +631,15 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     if (C > 32 && !g->epi_grp) return fail(PR_ERR_INVALID, "more than 32 column classes need the grouped epilogue (< 2^31 partial slots)");
     if (!g->epi_grp && !g->epi_abs && poff[C] >= (int64_t(1) << 31) - 4)
       return fail(PR_ERR_INVALID, "more than 2^31 partial slots");
-    // absolute first slots (grouped epilogue or k_epilogue<C, true>)
-    if (g->epi_abs || g->epi_grp)
-      for (int64_t blk = 0; blk < g->nblk; ++blk)
-        for (int x = 0; x < C; ++x) hbase[(size_t)blk * C + x] += (int32_t)poff[x];
-    // grouped epilogue: a sentinel row (block nblk) holds every class's end slot
-    if (g->epi_grp)
-      for (int x = 0; x < C; ++x) hbase.push_back((int32_t)poff[x + 1]);
     if (const char *e = getenv("PR_EPI_VAR")) g->epi_var = std::min(std::max(atoi(e), 0), kNumEpiVariants - 1);
-    wp.ucum.resize(kMaxClasses + 1, (int64_t)wp.units.size());
-    seg_p0.push_back((int32_t)pieces);
-    for (size_t q = 0; q < seg_slot.size(); ++q) seg_slot[q] += poff[seg_cls[q]];  // absolute partial slots
-    {
-      const int nw = (C + 31) / 32;
-      PR_TRY(g->rmask.alloc(sizeof(uint32_t) * (size_t)nw * ((size_t)R + 1)));
-      hipLaunchKernelGGL(k_row_masks, dim3(grid_for(R, T, 65536)), dim3(T), 0, s, R, C, nw, rp_all.as<int64_t>(),
-                         g->rmask.as<uint32_t>());
-    }
-    PR_HIP(hipGetLastError());
-    rp_all.reset();
-    if (wp.len / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
+    // per-block first slots: absolute (grouped epilogue, k_epilogue<C, true>) or class-local,
+    // plus the sentinel block row of every class's end slot
+    PR_TRY(sp.block_bases(g->epi_abs || g->epi_grp, s));
+    PR_TRY(sp.units_plan(s));
+    g->rmask = std::move(sp.rmask);
+    g->cbase = std::move(sp.cbase);
+    pieces = sp.n_pieces;
+    if (sp.entries / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
     // LDS hot set per class, then the entry codes
     const int slots = hot_slots_setting();
     HotGeom hg{};
@@ -794,59 +668,52 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->hot_phased = hot_phased_setting();
 
     PR_TRY(prepare_hot_kernel());
-    const size_t nu = wp.units.size();
-    g->n_hunits = (int64_t)nu;
-    PR_TRY(g->hunits.alloc(sizeof(Unit) * (nu + 1)));
-    PR_HIP(hipMemsetAsync(g->hunits.p, 0, sizeof(Unit) * (nu + 1), s));  // unit nu: the empty unit
+    const int64_t nu = sp.n_units;
+    g->n_hunits = nu;
+    g->hunits = std::move(sp.units);  // + the empty unit nu
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
-    PR_TRY(g->colh.alloc(sizeof(uint32_t) * (wp.len > 0 ? wp.len : 8)));
+    PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
     PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
-    PR_TRY(g->cbase.alloc(sizeof(int32_t) * (hbase.size() + 1)));
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
     g->n_slots = poff[C];
     for (int x = 0; x <= kMaxClasses; ++x) g->part_off.o[x] = poff[x];
-    PR_HIP(hipMemcpyAsync(g->hucum.p, wp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
+    PR_HIP(hipMemcpyAsync(g->hucum.p, sp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
-    if (!hbase.empty())
-      PR_HIP(hipMemcpyAsync(g->cbase.p, hbase.data(), sizeof(int32_t) * hbase.size(), hipMemcpyHostToDevice, s));
     if (nu > 0) {
-      DevBuf dsrc_off, dn;
-      PR_TRY(dsrc_off.alloc(sizeof(int64_t) * nu));
-      PR_TRY(dn.alloc(sizeof(int32_t) * nu));
-      PR_HIP(hipMemcpyAsync(g->hunits.p, wp.units.data(), sizeof(Unit) * nu, hipMemcpyHostToDevice, s));
-      PR_HIP(hipMemcpyAsync(dsrc_off.p, wp.src_off.data(), sizeof(int64_t) * nu, hipMemcpyHostToDevice, s));
-      PR_HIP(hipMemcpyAsync(dn.p, wp.n_real.data(), sizeof(int32_t) * nu, hipMemcpyHostToDevice, s));
-      hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(256), 0, s, (int64_t)nu,
-                         g->hunits.as<Unit>(), dsrc_off.as<int64_t>(), dn.as<int32_t>(), g->col.as<int32_t>(),
+      hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
+                         g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
                          hotidx.as<int32_t>(), g->colh.as<uint32_t>());
-      hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<size_t>(nu, 65536)), dim3(kWave), 0, s, (int64_t)nu,
+      hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(kWave), 0, s, nu,
                          g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
       PR_HIP(hipGetLastError());
       PR_HIP(hipStreamSynchronize(s));
     }
+    g->n_segs = sp.n_long;
+    g->seg_slot = std::move(sp.seg_slot);
+    g->seg_p0 = std::move(sp.seg_p0);
   }
   g->col.reset();
   if (lr_p0.empty()) lr_p0.push_back((int32_t)pieces);
   g->n_units = (int64_t)light_units.size();
   g->n_long = (int64_t)lr_row.size();
-  g->n_segs = (int64_t)seg_slot.size();
   g->n_pieces = pieces;
   PR_TRY(g->units.alloc(sizeof(Unit) * (light_units.size() + 1)));
   PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (lr_row.size() + 1)));
   PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (lr_p0.size() + 1)));
-  PR_TRY(g->seg_slot.alloc(sizeof(int64_t) * (seg_slot.size() + 1)));
-  PR_TRY(g->seg_p0.alloc(sizeof(int32_t) * (seg_p0.size() + 1)));
+  if (C == 1) {  // no long segments (the split planner filled these)
+    g->n_segs = 0;
+    PR_TRY(g->seg_slot.alloc(sizeof(int64_t)));
+    PR_TRY(g->seg_p0.alloc(sizeof(int32_t) * (seg_p0.size() + 1)));
+    PR_HIP(hipMemcpyAsync(g->seg_p0.p, seg_p0.data(), sizeof(int32_t) * seg_p0.size(), hipMemcpyHostToDevice, s));
+  }
   PR_TRY(g->piece_part.alloc(sizeof(double) * ((size_t)g->n_pieces + 1)));
   if (!light_units.empty())
     PR_HIP(hipMemcpyAsync(g->units.p, light_units.data(), sizeof(Unit) * light_units.size(), hipMemcpyHostToDevice, s));
   if (!lr_row.empty())
     PR_HIP(hipMemcpyAsync(g->lr_row.p, lr_row.data(), sizeof(int32_t) * lr_row.size(), hipMemcpyHostToDevice, s));
   PR_HIP(hipMemcpyAsync(g->lr_p0.p, lr_p0.data(), sizeof(int32_t) * lr_p0.size(), hipMemcpyHostToDevice, s));
-  if (!seg_slot.empty())
-    PR_HIP(hipMemcpyAsync(g->seg_slot.p, seg_slot.data(), sizeof(int64_t) * seg_slot.size(), hipMemcpyHostToDevice, s));
-  PR_HIP(hipMemcpyAsync(g->seg_p0.p, seg_p0.data(), sizeof(int32_t) * seg_p0.size(), hipMemcpyHostToDevice, s));
   g->orig_of_local.resize((size_t)R);
   if (R > 0)
     PR_HIP(hipMemcpyAsync(g->orig_of_local.data(), orig.p, sizeof(int32_t) * R, hipMemcpyDeviceToHost, s));

@@ -143,7 +143,7 @@ constexpr int kMetaExclShift = 14;
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
 // ~0.5 % and 64 by ~0.8 % at R-MAT s26, profiles/r01/stage_ab/).
 #ifndef PR_STAGE_SLOTS
-#define PR_STAGE_SLOTS 128  // other values: A/B builds only (tools/gpu/stage.sh)
+#define PR_STAGE_SLOTS 128  // other values: A/B builds only (-DPR_STAGE_SLOTS=...)
 #endif
 constexpr int kStageSlots = PR_STAGE_SLOTS;
 constexpr int kHotLdsBytes = 160 * 1024;

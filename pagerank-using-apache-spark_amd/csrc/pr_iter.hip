@@ -1,25 +1,26 @@
 // The PageRank power iteration on gfx950 (K3/K4 in SURVEY.md §2.1): the hot path.
 //
-// One iteration of Sparky.java:189-235 is two launches plus, for several parts, one RCCL
-// all-gather:
+// One iteration of Sparky.java:189-235 on one part (pr_graph.h layouts):
 //
-//   k_spmv_units (one workgroup per work unit; THE dominant kernel)
-//     STREAM unit: whole rows [r0, r0+nr) with <= 2048 in-links.  The in-link column stream is
-//       read coalesced (int32), each lane gathers 8 contributions c[u] = r(u)/d(u) into LDS
-//       (Sparky.java:192-216 join + flatMapToPair), then every thread reduces 8 consecutive
-//       LDS values along row boundaries with a wave64 segmented scan for rows that cross
-//       threads (reduceByKey(Sum), Sparky.java:27-32, :229) -- balanced whatever the row
-//       lengths.  The epilogue is coalesced over the unit's rows and fuses:
-//         in-degree-0 quirk: S = r_old              (subtractByKey + union, :224-225)
-//         r' = 0.15 + 0.85 * (S + dc / N)           (:233, no FMA contraction)
-//         c' = r' / d for the next iteration        (:207, a true division)
-//         partial sum of r' over sink-only rows     (danglingContrib of the next iteration, :219-222)
-//         partial L1 |r' - r|                        (convergence norm; reported only)
-//     PIECE unit: 2048 in-links of a long row -> one partial sum.
-//   k_finalize: long rows (sum of their pieces in piece order + the same epilogue), then a
-//     deterministic reduction of all unit partials into the two slots {dc partial, L1 partial}
-//     at the end of this part's gather slice (last-arriving workgroup, agent-scope sc1 protocol
-//     of cdna_hip_programming.md Guideline 16).
+//   split layout (C > 1 column classes; every graph whose gather space passes 4 MiB):
+//     k_spmv_hot     per class, the wave units of consecutive (row, class) segments: codes
+//                    address the class's LDS hot set or the gather space; per-lane sums and a
+//                    wave64 DPP segmented scan give one partial sum per segment
+//                    (join + flatMapToPair + the map side of reduceByKey, Sparky.java:192-216, :229)
+//     k_seg_reduce   long segments: their pieces summed in piece order
+//     k_epilogue_grp per row, its segment sums in class order (reduceByKey(Sum), :27-32, :229),
+//                    then the update fused:
+//                      in-degree-0 quirk: S = r_old             (subtractByKey + union, :224-225)
+//                      r' = 0.15 + 0.85 * (S + dc / N)          (:233, no FMA contraction)
+//                      c' = r' / d for the next iteration       (:207, a true division)
+//                      block partials of sum r' over sink rows  (danglingContrib, :219-222)
+//                      block partials of |r' - r|               (L1 convergence norm; reported only)
+//   fused layout (C = 1, small graphs): k_spmv_units does all of that in one launch per unit.
+//   k_finalize       long rows of the fused layout, then a deterministic reduction of all block
+//                    partials into the part's two slots {dc partial, L1 partial} at the end of
+//                    its gather slice (last-arriving workgroup, agent-scope protocol of
+//                    cdna_hip_programming.md Guideline 16).
+//   P > 1: the exchange (pr_exchange.hip) sends every peer the contributions its in-links read.
 //
 // Every sum has a fixed order, so results are bitwise reproducible run to run.
 #include <climits>

@@ -647,14 +647,23 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       rold[g] = ok ? r[L] : 0.0;
       S[g] = 0.0;
     }
-    // lane x < C holds class x's run [cs, ce) (read back per class with v_readlane)
+    // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
+    // per class with v_readlane
     const int cs = lane < C ? cbase[b0 * C + lane] : 0;
     const int ce = lane < C ? cbase[(b0 + nb) * C + lane] : 0;
+    const int cs1 = (C > kWave && lane + kWave < C) ? cbase[b0 * C + kWave + lane] : 0;
+    const int ce1 = (C > kWave && lane + kWave < C) ? cbase[(b0 + nb) * C + kWave + lane] : 0;
+    auto run_start = [&](int y) {
+      return (C <= kWave || y < kWave) ? __builtin_amdgcn_readlane(cs, y) : __builtin_amdgcn_readlane(cs1, y - kWave);
+    };
+    auto run_end = [&](int y) {
+      return (C <= kWave || y < kWave) ? __builtin_amdgcn_readlane(ce, y) : __builtin_amdgcn_readlane(ce1, y - kWave);
+    };
     for (int x = 0; x < C;) {
       // stage the runs of classes [x, xe) that fit the window (at least one always does)
       int fill = 0, xe = x;
       for (; xe < C; ++xe) {
-        const int s = __builtin_amdgcn_readlane(cs, xe), e = __builtin_amdgcn_readlane(ce, xe);
+        const int s = run_start(xe), e = run_end(xe);
         if (e == s) continue;  // no slots in this group
         const int sa = s & ~1, n2 = ((e + 1) & ~1) - sa;
         if (xe > x && fill + n2 > W) break;
@@ -666,7 +675,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
       fill = 0;
       for (int y = x; y < xe; ++y) {
-        const int s = __builtin_amdgcn_readlane(cs, y), e = __builtin_amdgcn_readlane(ce, y);
+        const int s = run_start(y), e = run_end(y);
         if (e == s) continue;
         const int sa = s & ~1;
         const uint32_t bit = 1u << (y & 31);

@@ -47,7 +47,7 @@ def main():
     print(f"graph {a.graph} s{a.scale}: V={V} E'={info['n_edges']} units={info['n_units']} "
           f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
     variants = []
-    for tok in a.variants.split(","):
+    for tok in a.variants.replace("+", ",").split(","):
         if ":" in tok:
             v, b = tok.split(":")
             variants.append((int(v), (1 << int(b)) - 1, tok))

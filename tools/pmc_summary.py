@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 CSVs from tools/profile.sh into profiles/-ready JSON.
+"""Summarise rocprofv3 CSVs from tools/gpu/run.sh (step pmc) into profiles/-ready JSON.
 
 usage: python tools/pmc_summary.py <prof_dir> <scale> [out_json]
 Reads <prof_dir>/trace/**/*kernel_stats.csv, <prof_dir>/fetch/**/*counter_collection.csv and

@@ -1,30 +1,35 @@
-"""Per-dispatch counter table for one kernel from rocprofv3 --pmc CSV passes (diagnostics).
+"""Per-kernel table of rocprofv3 counter CSVs (median over dispatches of each kernel).
 
-usage: python tools/pmc_table.py <dir-glob> <kernel-substring>
-Prints, per counter, the median over the kernel's dispatches of the counter summed over
-dimensions (XCC / SE / instance rows of one dispatch).
+usage: python tools/pmc_table.py <dir> [<dir> ...] [--kernels k_spmv_hot,k_epilogue]
 """
 import csv
 import glob
+import os
 import statistics
 import sys
 
 
 def main():
-    pat, kern = sys.argv[1], sys.argv[2]
-    per = {}
-    for path in sorted(glob.glob(pat + "/**/*counter_collection.csv", recursive=True)):
-        with open(path) as f:
-            for r in csv.DictReader(f):
-                if kern not in r.get("Kernel_Name", ""):
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    ks = ["k_spmv_hot", "k_epilogue", "k_seg_reduce"]
+    for a in sys.argv[1:]:
+        if a.startswith("--kernels="):
+            ks = a.split("=", 1)[1].split(",")
+    for d in args:
+        vals = {}
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(path)):
+                name = r.get("Kernel_Name", "")
+                k = next((k for k in ks if k in name), None)
+                if k is None:
                     continue
-                key = (r["Counter_Name"], r.get("Dispatch_Id") or r.get("Correlation_Id"))
-                per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
-    byc = {}
-    for (c, _), v in per.items():
-        byc.setdefault(c, []).append(v)
-    for c in sorted(byc):
-        print(f"{c:40s} {statistics.median(byc[c]):16.4g}  (n={len(byc[c])})")
+                key = (k, r["Counter_Name"])
+                disp = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                vals.setdefault(key, {}).setdefault(disp, 0.0)
+                vals[key][disp] += float(r["Counter_Value"])
+        print(f"== {d}")
+        for (k, c), per in sorted(vals.items()):
+            print(f"  {k:14s} {c:32s} {statistics.median(per.values()):18.1f}  (n={len(per)})")
 
 
 if __name__ == "__main__":
