@@ -172,12 +172,13 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // partial stores, 4 / 5 = gathers folded into 4 / 32 MiB (1, 2, 4, 5: diagnostics, results wrong);
 // 13 / 14 / 15 = variants 0 / 1 / 4 with the reduce of unit i before the gathers of i+1;
 // 16..19 = phased schedule (the product's): product, all-LDS, all-LDS + an out-of-range buffer
-// load per entry, gathers without LDS reads.  The hot-set size is a build setting
+// load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, non-temporal
+// partial stores, every gather folded into the first 4 MiB.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[20] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[23] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -196,8 +197,11 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 13, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 14, 1>)};
-  if (variant < 0 || variant > 19) return fail(PR_ERR_INVALID, "unknown variant");
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 14, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 2, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 3, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>)};
+  if (variant < 0 || variant > 22) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
