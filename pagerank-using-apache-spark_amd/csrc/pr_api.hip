@@ -196,6 +196,7 @@ int pr_step(pr_graph *g, int32_t iterations) {
 int pr_sync(pr_graph *g) {
   if (!g) return fail(PR_ERR_INVALID, "NULL graph");
   DeviceGuard dg(g->device);
+  PR_TRY(pr::join_exchange(g));  // an overlapped exchange still on xstream
   PR_HIP(hipStreamSynchronize(g->stream));
   return PR_OK;
 }
@@ -222,6 +223,7 @@ int pr_set_timing(pr_graph *g, int32_t enable) {
 int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
   if (!g || !stats) return fail(PR_ERR_INVALID, "NULL argument");
   DeviceGuard dg(g->device);
+  PR_TRY(pr::join_exchange(g));
   PR_HIP(hipStreamSynchronize(g->stream));
   auto mean_ms = [&](const std::vector<std::pair<int, int>> &ev, double *out) -> int {
     double acc = 0.0;
@@ -365,6 +367,7 @@ int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, dou
   PR_TRY(pr::group_exchange(parts, n_parts, 0));
   for (int32_t p = 0; p < n_parts; ++p) {
     PR_HIP(hipSetDevice(parts[p]->device));
+    PR_TRY(pr::join_exchange(parts[p]));
     PR_HIP(hipStreamSynchronize(parts[p]->stream));
   }
   return PR_OK;
@@ -389,6 +392,7 @@ int pr_group_sync(pr_graph *const *parts, int32_t n_parts) {
   PR_TRY(check_group(parts, n_parts));
   for (int32_t p = 0; p < n_parts; ++p) {
     PR_HIP(hipSetDevice(parts[p]->device));
+    PR_TRY(pr::join_exchange(parts[p]));
     PR_HIP(hipStreamSynchronize(parts[p]->stream));
   }
   return PR_OK;
@@ -398,9 +402,13 @@ void pr_graph_destroy(pr_graph *g) {
   if (!g) return;
   DeviceGuard dg(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
+  if (g->xstream) (void)hipStreamSynchronize(g->xstream);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
   if (g->xev) (void)hipEventDestroy(g->xev);
+  for (hipEvent_t e : g->x_ev) (void)hipEventDestroy(e);
+  if (g->x_pack_ev) (void)hipEventDestroy(g->x_pack_ev);
+  if (g->xstream) (void)hipStreamDestroy(g->xstream);
   g->ev_pool.clear();
   hipStream_t s = g->stream;
   g->stream = nullptr;

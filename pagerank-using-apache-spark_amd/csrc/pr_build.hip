@@ -537,6 +537,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
 
   // ---- exchange lists (P > 1): which of this part's contributions every peer reads ----
   DevBuf cmap;  // global -> compacted gather position (P > 1, sparse exchange)
+  g->hot_phased = C > 1 && hot_phased_setting();  // the exchange is chunked by hot phase
   PR_TRY(build_exchange(g, ukeys, m, b, maskb, rank_of.as<int32_t>(), gpos.as<int32_t>(), &cmap));
 
   // ---- the part's in-link CSRs: one per column class (one in the fused layout) ----

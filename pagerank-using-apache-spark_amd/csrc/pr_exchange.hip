@@ -121,6 +121,51 @@ __global__ void k_cmap_recv(int64_t n, const uint32_t *__restrict__ recv, int64_
     cmap[recv[k]] = (int32_t)(S_pad + k);
 }
 
+// Chunk starts of every peer's run (overlapped exchange): out[q * (nc + 1) + c] = index within
+// peer q's run [off[q], off[q + 1]) of its first position at or past the class regions of hot
+// phases < c (slice row 8 c Q_pad); out[q * (nc + 1) + nc] = the run length (the two slots, the
+// largest positions of a run, fall in the last chunk).  Receive lists hold global positions.
+__global__ void k_chunk_bounds(const uint32_t *__restrict__ list, const int64_t *__restrict__ off, int P, int self,
+                               int nc, int64_t row_stride, int64_t S_pad, bool send, int64_t *__restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= P * (nc + 1)) return;
+  const int q = t / (nc + 1), c = t - q * (nc + 1);
+  const int64_t b = off[q], e = off[q + 1];
+  int64_t r = 0;
+  if (q != self) {
+    if (c == nc) {
+      r = e - b;
+    } else if (c > 0) {
+      const int64_t base = send ? 0 : (int64_t)q * S_pad, target = (int64_t)c * row_stride;
+      int64_t lo = b, hi = e;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)list[mid] - base < target) lo = mid + 1;
+        else hi = mid;
+      }
+      r = lo - b;
+    }
+  }
+  out[t] = r;
+}
+
+int chunk_bounds(pr_graph *g, const uint32_t *list, const std::vector<int64_t> &off, bool send,
+                 std::vector<int64_t> *out) {
+  const int P = g->nparts, nc = g->n_xc;
+  hipStream_t s = g->stream;
+  DevBuf doff, dout;
+  PR_TRY(doff.alloc(sizeof(int64_t) * (P + 1)));
+  PR_TRY(dout.alloc(sizeof(int64_t) * P * (nc + 1)));
+  PR_HIP(hipMemcpyAsync(doff.p, off.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_chunk_bounds, dim3((P * (nc + 1) + 255) / 256), dim3(256), 0, s, list, doff.as<int64_t>(), P,
+                     g->part, nc, (int64_t)kXcds * g->Q_pad, g->S_pad, send, dout.as<int64_t>());
+  PR_HIP(hipGetLastError());
+  out->assign((size_t)P * (nc + 1), 0);
+  PR_HIP(hipMemcpyAsync(out->data(), dout.p, sizeof(int64_t) * P * (nc + 1), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  return PR_OK;
+}
+
 bool allgather_requested() {
   const char *e = getenv("PR_EXCHANGE");
   return e && std::strcmp(e, "allgather") == 0;
@@ -204,6 +249,17 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   // runs of iteration k may still be pending when this part packs iteration k + 1
   PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
   PR_HIP(hipStreamSynchronize(s));
+  // chunks of the overlapped exchange: one per hot phase (PR_XCHG_CHUNKS=0: one chunk, i.e. the
+  // next iteration waits for the whole exchange -- the A/B reference)
+  g->n_xc = (g->C > 1 && g->hot_phased) ? std::max(1, g->C / kXcds) : 1;
+  if (const char *e = getenv("PR_XCHG_CHUNKS"))
+    if (atoi(e) == 0) g->n_xc = 1;
+  PR_TRY(chunk_bounds(g, g->x_send.as<uint32_t>(), g->x_soff, true, &g->x_sch));
+  PR_TRY(chunk_bounds(g, recv.as<uint32_t>(), g->x_roff, false, &g->x_rch));
+  PR_HIP(hipStreamCreateWithFlags(&g->xstream, hipStreamNonBlocking));
+  g->x_ev.assign(g->n_xc, nullptr);
+  for (auto &e : g->x_ev) PR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  PR_HIP(hipEventCreateWithFlags(&g->x_pack_ev, hipEventDisableTiming));
   return PR_OK;
 }
 
@@ -222,11 +278,12 @@ int exchange_pack(pr_graph *g, int buf) {
 // desynchronising the send/receive pairs.
 int verify_exchange(pr_graph *g) {
   const int P = g->nparts;
-  const int W = P + 3;
+  const int W = P + 4;
   std::vector<int64_t> mine(W, 0);
   mine[0] = g->V;
   mine[1] = g->S_pad;
   mine[2] = g->x_allgather ? 1 : 0;
+  mine[P + 3] = g->n_xc;  // chunking of the overlapped exchange (PR_XCHG_CHUNKS, PR_HOT_PHASED)
   if (!g->x_allgather)
     for (int q = 0; q < P; ++q) mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
   DevBuf d;
@@ -241,70 +298,99 @@ int verify_exchange(pr_graph *g) {
     const int64_t *o = all.data() + (size_t)q * W;
     if (o[0] != g->V || o[1] != g->S_pad) return fail(PR_ERR_INVALID, "ranks hold parts of different graphs");
     if (o[2] != mine[2]) return fail(PR_ERR_INVALID, "ranks disagree on PR_EXCHANGE");
+    if (o[P + 3] != mine[P + 3]) return fail(PR_ERR_INVALID, "ranks disagree on the exchange chunking");
     if (q != g->part && !g->x_allgather && o[3 + g->part] != g->x_roff[q + 1] - g->x_roff[q])
       return fail(PR_ERR_STATE, "exchange lists disagree between ranks");
   }
   return PR_OK;
 }
 
-// One process per GPU (RCCL).
-int exchange(pr_graph *g, int buf) {
+// One process per GPU (RCCL).  Whole slices: one in-place ncclAllGather on the compute stream.
+// Runs: the pack runs on the compute stream; the n_xc chunks of every peer's run go out as
+// grouped ncclSend / ncclRecv on xstream, x_ev[c] after chunk c (the next iteration's hot phase c
+// waits for it: iter_compute).  ev_a / ev_b (may be null): timing events around the transfer.
+int exchange(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   if (g->nparts <= 1) return PR_OK;
   if (!g->comm) return fail(PR_ERR_STATE, "graph part has no communicator (pr_graph_attach_comm)");
   double *base = g->cbuf[buf].as<double>();
   if (g->x_allgather) {  // whole slices, in place
+    if (ev_a) PR_HIP(hipEventRecord(ev_a, g->stream));
     ncclResult_t rc = ncclAllGather(base + (int64_t)g->part * g->S_pad, base, (size_t)g->S_pad, ncclDouble, g->comm,
                                     g->stream);
     if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+    if (ev_b) PR_HIP(hipEventRecord(ev_b, g->stream));
     return PR_OK;
   }
   PR_TRY(exchange_pack(g, buf));
-  ncclResult_t rc = ncclGroupStart();
-  for (int q = 0; q < g->nparts && rc == ncclSuccess; ++q) {
-    if (q == g->part) continue;
-    rc = ncclSend(send_runs(g, buf) + g->x_soff[q], (size_t)(g->x_soff[q + 1] - g->x_soff[q]), ncclDouble, q,
-                  g->comm, g->stream);
-    if (rc == ncclSuccess)
-      rc = ncclRecv(base + g->S_pad + g->x_roff[q], (size_t)(g->x_roff[q + 1] - g->x_roff[q]), ncclDouble, q,
-                    g->comm, g->stream);
+  PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
+  PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
+  if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
+  const int nc = g->n_xc;
+  const double *sruns = send_runs(g, buf);
+  for (int c = 0; c < nc; ++c) {
+    ncclResult_t rc = ncclGroupStart();
+    for (int q = 0; q < g->nparts && rc == ncclSuccess; ++q) {
+      if (q == g->part) continue;
+      const int64_t s0 = g->x_sch[(size_t)q * (nc + 1) + c], s1 = g->x_sch[(size_t)q * (nc + 1) + c + 1];
+      const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + c], r1 = g->x_rch[(size_t)q * (nc + 1) + c + 1];
+      // both ends derive the chunk sizes from the same positions: a zero-size pair is skipped on both
+      if (s1 > s0) rc = ncclSend(sruns + g->x_soff[q] + s0, (size_t)(s1 - s0), ncclDouble, q, g->comm, g->xstream);
+      if (rc == ncclSuccess && r1 > r0)
+        rc = ncclRecv(base + g->S_pad + g->x_roff[q] + r0, (size_t)(r1 - r0), ncclDouble, q, g->comm, g->xstream);
+    }
+    const ncclResult_t rc2 = ncclGroupEnd();
+    if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(rc));
+    if (rc2 != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(rc2));
+    PR_HIP(hipEventRecord(g->x_ev[c], g->xstream));
   }
-  const ncclResult_t rc2 = ncclGroupEnd();
-  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(rc));
-  if (rc2 != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(rc2));
+  if (ev_b) PR_HIP(hipEventRecord(ev_b, g->xstream));
+  g->x_pending = true;
   return PR_OK;
 }
 
-// One process, several parts: the same packed runs moved by device copies (peer copies over xGMI
-// when the parts live on different GPUs), pulled by the receiver on its stream after p's pack.
-// p's next pack goes to its other send buffer; the one after that is ordered behind q's copies
-// by p's wait on q's event in the next exchange.  q's gather space is only written on q's
-// stream.
+// One process, several parts: the same packed runs, chunk by chunk, moved by device copies (peer
+// copies over xGMI when the parts live on different GPUs) on the receiver's xstream after every
+// part's pack (its own included: the copies overwrite gather space its previous iteration read).
+// p's next pack goes to its other send buffer; the one after that is ordered behind q's copies:
+// q's next iteration waits for them before its pack, and p waits for q's pack.
 int group_exchange(pr_graph *const *parts, int n, int buf) {
   if (n <= 1) return PR_OK;
   const bool whole = parts[0]->x_allgather;
   for (int p = 0; p < n; ++p) {
     PR_HIP(hipSetDevice(parts[p]->device));
     if (!whole) PR_TRY(exchange_pack(parts[p], buf));
-    PR_HIP(hipEventRecord(parts[p]->xev, parts[p]->stream));
+    PR_HIP(hipEventRecord(whole ? parts[p]->xev : parts[p]->x_pack_ev, parts[p]->stream));
   }
   for (int q = 0; q < n; ++q) {
     pr_graph *g = parts[q];
     PR_HIP(hipSetDevice(g->device));
-    for (int p = 0; p < n; ++p) {
-      if (p == q) continue;
-      PR_HIP(hipStreamWaitEvent(g->stream, parts[p]->xev, 0));
-      if (whole) {
+    if (whole) {  // whole slices on the compute stream (the A/B reference)
+      for (int p = 0; p < n; ++p) {
+        if (p == q) continue;
+        PR_HIP(hipStreamWaitEvent(g->stream, parts[p]->xev, 0));
         const int64_t off = (int64_t)p * g->S_pad;
         PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + off, parts[p]->cbuf[buf].as<double>() + off,
                               sizeof(double) * g->S_pad, hipMemcpyDeviceToDevice, g->stream));
-      } else {
-        const pr_graph *src = parts[p];
-        const int64_t cnt = g->x_roff[p + 1] - g->x_roff[p];
-        if (cnt != src->x_soff[q + 1] - src->x_soff[q]) return fail(PR_ERR_STATE, "exchange lists disagree");
-        PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + g->S_pad + g->x_roff[p], send_runs(src, buf) + src->x_soff[q],
-                              sizeof(double) * cnt, hipMemcpyDeviceToDevice, g->stream));
       }
+      continue;
     }
+    for (int p = 0; p < n; ++p) PR_HIP(hipStreamWaitEvent(g->xstream, parts[p]->x_pack_ev, 0));
+    const int nc = g->n_xc;
+    for (int c = 0; c < nc; ++c) {
+      for (int p = 0; p < n; ++p) {
+        if (p == q) continue;
+        const pr_graph *src = parts[p];
+        const int64_t r0 = g->x_rch[(size_t)p * (nc + 1) + c], r1 = g->x_rch[(size_t)p * (nc + 1) + c + 1];
+        const int64_t s0 = src->x_sch[(size_t)q * (nc + 1) + c], s1 = src->x_sch[(size_t)q * (nc + 1) + c + 1];
+        if (r1 - r0 != s1 - s0) return fail(PR_ERR_STATE, "exchange lists disagree");
+        if (r1 > r0)
+          PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + g->S_pad + g->x_roff[p] + r0,
+                                send_runs(src, buf) + src->x_soff[q] + s0, sizeof(double) * (r1 - r0),
+                                hipMemcpyDeviceToDevice, g->xstream));
+      }
+      PR_HIP(hipEventRecord(g->x_ev[c], g->xstream));
+    }
+    g->x_pending = true;
   }
   return PR_OK;
 }

@@ -104,6 +104,21 @@ struct pr_graph {
   pr::DevBuf x_send, x_sbuf;
   std::vector<int64_t> x_soff, x_roff;
   bool x_allgather = false;  // PR_EXCHANGE=allgather: whole slices instead
+  // Overlapped exchange (P > 1, split layout, phased k_spmv_hot): every peer's run is sent in
+  // n_xc chunks on xstream, chunk c = its positions in the class regions of hot phase c (classes
+  // [8c, 8c + 8)), the last chunk also carrying the two slots (a run is sorted by position, so
+  // the chunks are consecutive pieces of it).  x_sch / x_rch[peer * (n_xc + 1) + c]: chunk starts
+  // within the peer's send / receive run.  x_ev[c] is recorded after chunk c; while x_pending,
+  // the next iteration's phase c waits for x_ev[c] only (pr_iter.hip), so the transfer of the
+  // later classes overlaps the SpMV of the earlier ones.
+  int n_xc = 1;
+  std::vector<int64_t> x_sch, x_rch;
+  hipStream_t xstream = nullptr;
+  std::vector<hipEvent_t> x_ev;
+  hipEvent_t x_pack_ev = nullptr, x_t0 = nullptr, x_t1 = nullptr;
+  bool x_pending = false;
+  int x_timed = 0;  // exchanges timed on xstream (x_t0 -> x_t1 of the last one)
+  double x_ms_sum = 0.0;
 
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
@@ -119,7 +134,10 @@ namespace pr {
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
-int launch_hot(pr_graph *g, int in_buf);  // the heavy-row pass (k_spmv_hot) on g's stream
+// the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
+int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);
+int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange
+int n_hot_phases(const pr_graph *g);
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
 int group_exchange(pr_graph *const *parts, int n, int buf);
@@ -127,7 +145,7 @@ int group_exchange(pr_graph *const *parts, int n, int buf);
 // global -> compacted position map (-1: not read by this part) when the space is compacted.
 int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
                    const int32_t *gpos, DevBuf *cmap);
-int exchange(pr_graph *g, int buf);
+int exchange(pr_graph *g, int buf, hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
 }  // namespace pr

@@ -163,20 +163,31 @@ int prepare_hot_kernel() {
   return PR_OK;
 }
 
-int launch_hot(pr_graph *g, int in) {
+int n_hot_phases(const pr_graph *g) { return g->hot_phased ? std::max(1, g->C / kXcds) : 1; }
+
+int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   const size_t lds = g->hot.lds_bytes();
   auto *kern = g->hot_phased ? &k_spmv_hot<0, 0, 1> : &k_spmv_hot<0, 0, 0>;
+  if (ph1 < 0) ph1 = n_hot_phases(g);
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
                      g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),
-                     g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>());
+                     g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+
+int join_exchange(pr_graph *g) {
+  if (!g->x_pending) return PR_OK;
+  PR_HIP(hipStreamWaitEvent(g->stream, g->x_ev.back(), 0));  // chunks are recorded in order
+  g->x_pending = false;
   return PR_OK;
 }
 
 int iter_reset(pr_graph *g, const double *init_host) {
   hipStream_t s = g->stream;
+  PR_TRY(join_exchange(g));  // a previous run's exchange may still be on xstream
   DevBuf dinit;
   if (init_host && g->n_rows > 0) {
     std::vector<double> loc((size_t)g->n_rows, 0.0);
@@ -193,7 +204,10 @@ int iter_reset(pr_graph *g, const double *init_host) {
                      g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
   PR_HIP(hipGetLastError());
   PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0));
-  if (!g->grouped) PR_TRY(exchange(g, 0));
+  if (!g->grouped) {
+    PR_TRY(exchange(g, 0));
+    PR_TRY(join_exchange(g));
+  }
   PR_HIP(hipStreamSynchronize(s));
   g->iters_done = 0;
   g->ready = true;
@@ -216,6 +230,7 @@ int iter_compute(pr_graph *g) {
     PR_HIP(hipEventRecord(e0, s));
   }
   // light rows (all rows when C == 1): fused single pass
+  if (g->C == 1) PR_TRY(join_exchange(g));
   if (g->n_units > 0)
     hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
@@ -224,7 +239,18 @@ int iter_compute(pr_graph *g) {
                        g->slots, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
   int64_t n_parts = g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
-    if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
+    const int nph = n_hot_phases(g);
+    if (g->n_hunits > 0 && g->x_pending && g->n_xc == nph && nph > 1) {
+      // overlapped exchange: hot phase c needs only chunk c of the runs received from every peer
+      for (int c = 0; c < nph; ++c) {
+        PR_HIP(hipStreamWaitEvent(s, g->x_ev[c], 0));
+        PR_TRY(launch_hot(g, in, c, c + 1));
+      }
+      g->x_pending = false;
+    } else {
+      PR_TRY(join_exchange(g));
+      if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
+    }
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
@@ -264,7 +290,7 @@ int iter_step(pr_graph *g, int32_t iterations) {
   if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
   if (g->grouped) return fail(PR_ERR_STATE, "graph belongs to a group: use pr_group_step");
   for (int32_t it = 0; it < iterations; ++it) {
-    hipEvent_t e0 = nullptr, e1 = nullptr, x0 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g->timing) {
       e0 = next_event(g);
       if (!e0) return fail(PR_ERR_HIP, "hipEventCreate failed");
@@ -272,18 +298,20 @@ int iter_step(pr_graph *g, int32_t iterations) {
     }
     const int i0 = (int)g->ev_next - 1;
     PR_TRY(iter_compute(g));
-    if (g->timing) {
-      x0 = next_event(g);
-      if (!x0) return fail(PR_ERR_HIP, "hipEventCreate failed");
-      PR_HIP(hipEventRecord(x0, g->stream));
+    hipEvent_t xa = nullptr, xb = nullptr;
+    if (g->timing && g->nparts > 1) {
+      xa = next_event(g);
+      xb = next_event(g);
+      if (!xa || !xb) return fail(PR_ERR_HIP, "hipEventCreate failed");
+      const int ia = (int)g->ev_next - 2;
+      g->xchg_ev.push_back({ia, ia + 1});  // pack done -> last chunk received (xstream)
     }
-    PR_TRY(exchange(g, g->cur));
+    PR_TRY(exchange(g, g->cur, xa, xb));
     if (g->timing) {
       e1 = next_event(g);
       if (!e1) return fail(PR_ERR_HIP, "hipEventCreate failed");
-      PR_HIP(hipEventRecord(e1, g->stream));
+      PR_HIP(hipEventRecord(e1, g->stream));  // compute stream: the iteration's kernels + the pack
       const int i1 = (int)g->ev_next - 1;
-      g->xchg_ev.push_back({i1 - 1, i1});
       g->iter_ev.push_back({i0, i1});
     }
   }
@@ -291,6 +319,7 @@ int iter_step(pr_graph *g, int32_t iterations) {
 }
 
 int read_slots(pr_graph *g, int buf, double *dc, double *l1) {
+  PR_TRY(join_exchange(g));  // the peers' slots arrive with the exchange
   std::vector<double> h(2 * (size_t)g->nparts);
   for (int p = 0; p < g->nparts; ++p)
     PR_HIP(hipMemcpyAsync(&h[2 * p], g->cbuf[buf].as<double>() + g->slots.pos[p], 2 * sizeof(double),

@@ -305,7 +305,7 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *_
 }
 
 // DIAG (diagnostics library only; results wrong when != 0): 1 = every value from LDS (no
-// gather-space loads), 2 = no partial stores, 3 = non-temporal partial stores, 4 / 5 = every
+// gather-space loads), 2 = no partial stores, 3 = temporal (default-policy) partial stores, 4 / 5 = every
 // gather-space load folded into the first 4 / 32 MiB (L2- / Infinity-Cache-resident), 6 =
 // exec-masked gathers, 8 = every gather instruction reads 512 contiguous bytes, 13 = every value
 // from LDS plus an out-of-range buffer load per entry, 14 = no LDS reads (gathers only).
@@ -391,8 +391,11 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     const int n = min(kStageSlots, nseg - base);
     for (int i = lane_id(); i < n; i += kWave) {
       const uint32_t o = (uint32_t)(u.r0 + base + i) * 8u;
+      // non-temporal (nt): the partials are read back by the epilogue only after every class
+      // has run, so they should not evict the class region from L2 (5 % of the kernel at s26;
+      // DIAG 3 = the temporal stores of round 1, profiles/r02/experiments.md)
       if constexpr (DIAG != 2)
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i]), prs, o, 0, DIAG == 3 ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i]), prs, o, 0, DIAG == 3 ? 0 : 2);
     }
   }
 }
@@ -464,20 +467,21 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           double *__restrict__ partial,
                                                           const int64_t *__restrict__ poff,
                                                           double *__restrict__ piece_part,
-                                                          const int32_t *__restrict__ hpos) {
+                                                          const int32_t *__restrict__ hpos, int ph0, int ph1) {
   extern __shared__ double hot[];
   const int nh = hg.P * hg.Kp;
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
-  const int n_phase = PHASED ? hg.C / kXcds : 1;
-  for (int ph = 0; ph < n_phase; ++ph) {
+  // PHASED: phases [ph0, ph1) of this launch (one launch per phase when the exchange overlaps)
+  const int p_lo = PHASED ? ph0 : 0, p_hi = PHASED ? ph1 : 1;
+  for (int ph = p_lo; ph < p_hi; ++ph) {
     int x, team, nteams;
     if constexpr (PHASED) {
       x = (int)(blockIdx.x % kXcds) + kXcds * ph;
       team = (int)(blockIdx.x / kXcds);
       nteams = (int)(gridDim.x / kXcds);
-      if (ph > 0) __syncthreads();  // every wave is done with the previous class's hot set
+      if (ph > p_lo) __syncthreads();  // every wave is done with the previous class's hot set
     } else {
       x = (int)(blockIdx.x % kXcds) + kXcds * (int)((blockIdx.x / kXcds) % (hg.C / kXcds));
       team = (int)(blockIdx.x / hg.C);

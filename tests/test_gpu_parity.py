@@ -465,3 +465,38 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode, monkeyp
     finally:
         for p in parts:
             p.close()
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
+    """The overlapped exchange (pr_exchange.hip): with 64 classes the phased k_spmv_hot runs 8
+    phases and every peer's run travels in 8 chunks, chunk c = the positions of classes [8c, 8c+8);
+    the next iteration's phase c waits only for chunk c.  Against the oracle, and bitwise equal to
+    the same parts exchanging whole runs before the next iteration starts (PR_XCHG_CHUNKS=0): the
+    chunking moves the same values, only earlier."""
+    monkeypatch.setenv("PR_CLASSES", "64")
+    monkeypatch.setenv("PR_HOT_SLOTS", "600")
+    rng = np.random.default_rng(60 + P)
+    V = 60000
+    src, dst = random_edges(rng, V, 700000, hub_frac=0.02)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 9)
+    out = {}
+    for chunks in ("on", "off"):
+        if chunks == "off":
+            monkeypatch.setenv("PR_XCHG_CHUNKS", "0")
+        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split")
+                 for p in range(P)]
+        try:
+            assert all(p.info()["classes"] == 64 for p in parts)
+            grp = hip.PartGroup(parts)
+            grp.reset()
+            grp.step(4)
+            grp.step(5)  # a second pr_group_step starts with chunks still pending
+            grp.sync()
+            out[chunks] = grp.ranks()
+        finally:
+            for p in parts:
+                p.close()
+    assert np.array_equal(out["on"], out["off"])
+    assert max_rel(out["on"], ref["ranks"]) <= RANK_TOL

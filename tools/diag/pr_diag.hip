@@ -214,7 +214,8 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   int64_t *poff = g->poff.as<int64_t>();
   int32_t *hpos = g->hpos.as<int32_t>();
   // must match k_spmv_hot's parameter list exactly
-  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &poff, &pp, &hpos};
+  int ph0 = 0, ph1 = g->C / kXcds;
+  void *args[] = {&units, &ucum, &hg, &colh, &hmeta, &cin, (void *)&cin_bytes, &partial, &poff, &pp, &hpos, &ph0, &ph1};
   hipEvent_t a, b;
   PR_HIP(hipEventCreate(&a));
   PR_HIP(hipEventCreate(&b));
