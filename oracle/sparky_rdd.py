@@ -29,6 +29,7 @@ unspecified (Sparky.java:219-222, :229); this oracle uses exactly rounded sums
 from __future__ import annotations
 
 import math
+import re
 from collections import OrderedDict
 from typing import Dict, Hashable, Iterable, List, Optional, Sequence, Tuple
 
@@ -174,10 +175,6 @@ class _Num(str):
     """A JSON number kept as its source text (Gson's LazilyParsedNumber prints it verbatim)."""
 
 
-def _reject_constant(name):
-    raise ValueError(f"non-JSON constant {name}")
-
-
 def _gson_str(s: str) -> str:
     """JsonWriter.value(String) with htmlSafe = false (JsonElement.toString())."""
     out = ['"']
@@ -235,11 +232,164 @@ def gson_to_string(v) -> str:
     return "{" + ",".join(parts) + "}"
 
 
-def _parse_json(text: str):
-    import json
+_NOT_LITERAL = set("/\\;#={}[]:, \t\f\r\n")
+_ESCAPES = {'"': '"', "'": "'", "\\": "\\", "/": "/", "b": "\b", "f": "\f", "n": "\n", "r": "\r", "t": "\t",
+            "\n": "\n"}
+_NUMBER = re.compile(r"-?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?\Z")
 
-    return json.loads(text, object_pairs_hook=lambda p: ("obj", p), parse_int=_Num,
-                      parse_float=_Num, parse_constant=_reject_constant)
+
+def _parse_json(text: str):
+    """Gson's lenient JsonReader as Sparky.java:87 `new JsonParser().parse(String)` runs it:
+    comments (//, # to the end of the line; /* */), single-quoted and unquoted names and strings,
+    '=' / '=>' for ':', ';' for ',', an omitted array element read as null, the ")]}'\n"
+    prefix, one top-level value.  Unquoted literal: keyword (true/false/null, each letter in
+    either case) / JSON number (no leading zeros) / else string.  Restated from Gson's published
+    JsonReader rules (version unpinned): lenient inputs are parity-unpinned.
+    Objects: ("obj", [(key, value), ...]); numbers: _Num (source text)."""
+    n = len(text)
+    pos = [5 if text.startswith(")]}'\n") else 0]
+
+    def fail(msg):
+        raise ValueError(f"JSON: {msg} at {pos[0]}")
+
+    def ws():
+        i = pos[0]
+        while i < n:
+            c = text[i]
+            if c in " \t\n\r":
+                i += 1
+            elif c == "#" or text.startswith("//", i):
+                while i < n and text[i] != "\n":
+                    i += 1
+            elif text.startswith("/*", i):
+                j = text.find("*/", i + 2)
+                if j < 0:
+                    pos[0] = i
+                    fail("unterminated comment")
+                i = j + 2
+            else:
+                break
+        pos[0] = i
+
+    def string(quote):
+        i = pos[0] + 1
+        out = []
+        while True:
+            if i >= n:
+                fail("unterminated string")
+            c = text[i]
+            i += 1
+            if c == quote:
+                pos[0] = i
+                return "".join(out)
+            if c != "\\":
+                out.append(c)
+                continue
+            if i >= n:
+                fail("bad escape")
+            x = text[i]
+            i += 1
+            if x == "u":
+                h = text[i:i + 4]
+                if len(h) < 4 or any(ch not in "0123456789abcdefABCDEF" for ch in h):
+                    fail("bad \\u escape")
+                v = int(h, 16)
+                i += 4
+                if 0xD800 <= v < 0xDC00 and text.startswith("\\u", i):
+                    h2 = text[i + 2:i + 6]
+                    if len(h2) == 4 and all(ch in "0123456789abcdefABCDEF" for ch in h2) and 0xDC00 <= int(h2, 16) < 0xE000:
+                        v = 0x10000 + ((v - 0xD800) << 10) + (int(h2, 16) - 0xDC00)
+                        i += 6
+                out.append(chr(v))
+            elif x in _ESCAPES:
+                out.append(_ESCAPES[x])
+            else:
+                fail("bad escape")
+
+    def unquoted():
+        i = j = pos[0]
+        while j < n and text[j] not in _NOT_LITERAL:
+            j += 1
+        if j == i:
+            fail("expected value")
+        pos[0] = j
+        return text[i:j]
+
+    def keyword(s, word):
+        return len(s) == len(word) and all(a in (b, b.upper()) for a, b in zip(s, word))
+
+    def value(depth):
+        if depth > 512:
+            fail("nesting too deep")
+        ws()
+        if pos[0] >= n:
+            fail("unexpected end")
+        c = text[pos[0]]
+        if c == "{":
+            pos[0] += 1
+            pairs = []
+            ws()
+            if pos[0] < n and text[pos[0]] == "}":
+                pos[0] += 1
+                return ("obj", pairs)
+            while True:
+                ws()
+                if pos[0] >= n or text[pos[0]] == "}":
+                    fail("expected name")
+                k = string(text[pos[0]]) if text[pos[0]] in "\"'" else unquoted()
+                ws()
+                if pos[0] < n and text[pos[0]] == ":":
+                    pos[0] += 1
+                elif pos[0] < n and text[pos[0]] == "=":
+                    pos[0] += 2 if text.startswith("=>", pos[0]) else 1
+                else:
+                    fail("expected ':'")
+                pairs.append((k, value(depth + 1)))
+                ws()
+                if pos[0] < n and text[pos[0]] in ",;":
+                    pos[0] += 1
+                    continue
+                if pos[0] < n and text[pos[0]] == "}":
+                    pos[0] += 1
+                    return ("obj", pairs)
+                fail("expected ',' or '}'")
+        if c == "[":
+            pos[0] += 1
+            arr = []
+            ws()
+            if pos[0] < n and text[pos[0]] == "]":
+                pos[0] += 1
+                return arr
+            while True:
+                ws()
+                if pos[0] < n and text[pos[0]] in ",;]":
+                    arr.append(None)  # an omitted element is null (lenient)
+                else:
+                    arr.append(value(depth + 1))
+                ws()
+                if pos[0] < n and text[pos[0]] in ",;":
+                    pos[0] += 1
+                    continue
+                if pos[0] < n and text[pos[0]] == "]":
+                    pos[0] += 1
+                    return arr
+                fail("expected ',' or ']'")
+        if c in "\"'":
+            return string(c)
+        lit = unquoted()
+        if keyword(lit, "true"):
+            return True
+        if keyword(lit, "false"):
+            return False
+        if keyword(lit, "null"):
+            return None
+        return _Num(lit) if _NUMBER.match(lit) else lit
+
+    v = value(0)
+    ws()
+    if pos[0] != n:
+        fail("trailing characters")
+    return v
 
 
 def _get(obj, key):

@@ -105,12 +105,21 @@ struct JVal {
   }
 };
 
+// Gson's lenient JsonReader (Sparky.java:87 `new JsonParser().parse(String)` parses leniently):
+// comments (// and # to the end of the line, /* */), 'single-quoted' and unquoted names and
+// strings, '=' or '=>' for ':', ';' for ',', a missing array element read as null ("[1,,2]",
+// "[1,]"), the ")]}'\n" non-execute prefix; one top-level value.  An unquoted literal is a
+// keyword (true/false/null, each letter in either case), a JSON number (no leading zeros), or
+// else a string.  Restated from Gson's published JsonReader documentation and behaviour; the
+// reference's Gson version is unpinned, so lenient inputs are parity-unpinned.
 class JParser {
  public:
   JParser(const char *p, const char *e) : p_(p), e_(e) {}
   bool parse(JVal &out) {
+    static const char kPrefix[] = ")]}'\n";
+    if ((size_t)(e_ - p_) >= 5 && std::memcmp(p_, kPrefix, 5) == 0) p_ += 5;
     if (!value(out, 0)) return false;
-    ws();
+    if (!ws()) return false;
     if (p_ != e_) return err("trailing characters");
     return true;
   }
@@ -122,14 +131,32 @@ class JParser {
     if (error.empty()) error = m;
     return false;
   }
-  void ws() {
-    while (p_ < e_ && (*p_ == ' ' || *p_ == '\t' || *p_ == '\n' || *p_ == '\r')) ++p_;
-  }
-  bool lit(const char *w) {
-    size_t n = std::strlen(w);
-    if ((size_t)(e_ - p_) < n || std::memcmp(p_, w, n) != 0) return err("bad literal");
-    p_ += n;
+  bool ws() {  // whitespace and comments
+    while (p_ < e_) {
+      const char c = *p_;
+      if (c == ' ' || c == '\t' || c == '\n' || c == '\r') {
+        ++p_;
+      } else if (c == '#' || (c == '/' && p_ + 1 < e_ && p_[1] == '/')) {
+        while (p_ < e_ && *p_ != '\n') ++p_;
+      } else if (c == '/' && p_ + 1 < e_ && p_[1] == '*') {
+        const char *q = p_ + 2;
+        while (q + 1 < e_ && !(q[0] == '*' && q[1] == '/')) ++q;
+        if (q + 1 >= e_) return err("unterminated comment");
+        p_ = q + 2;
+      } else {
+        break;
+      }
+    }
     return true;
+  }
+  static bool literal_char(char c) {  // Gson JsonReader.isLiteral
+    switch (c) {
+      case '/': case '\\': case ';': case '#': case '=': case '{': case '}': case '[': case ']':
+      case ':': case ',': case ' ': case '\t': case '\f': case '\r': case '\n':
+        return false;
+      default:
+        return true;
+    }
   }
   static void put_utf8(std::string &o, uint32_t cp) {
     if (cp < 0x80) o.push_back((char)cp);
@@ -158,18 +185,18 @@ class JParser {
     }
     return true;
   }
-  bool string(std::string &o) {
+  bool string(std::string &o, char quote) {
     ++p_;  // opening quote
     while (true) {
       if (p_ >= e_) return err("unterminated string");
       char c = *p_++;
-      if (c == '"') return true;
-      if ((unsigned char)c < 0x20) return err("control character in string");
+      if (c == quote) return true;
       if (c != '\\') { o.push_back(c); continue; }
       if (p_ >= e_) return err("bad escape");
       char x = *p_++;
       switch (x) {
         case '"': o.push_back('"'); break;
+        case '\'': o.push_back('\''); break;
         case '\\': o.push_back('\\'); break;
         case '/': o.push_back('/'); break;
         case 'b': o.push_back('\b'); break;
@@ -177,6 +204,7 @@ class JParser {
         case 'n': o.push_back('\n'); break;
         case 'r': o.push_back('\r'); break;
         case 't': o.push_back('\t'); break;
+        case '\n': o.push_back('\n'); break;  // Gson: an escaped line break is the line break
         case 'u': {
           uint32_t v;
           if (!hex4(v)) return false;
@@ -195,40 +223,69 @@ class JParser {
       }
     }
   }
-  bool number(JVal &o) {
+  // an unquoted literal: the longest run of literal characters
+  bool unquoted(std::string &o) {
     const char *b = p_;
-    if (p_ < e_ && *p_ == '-') ++p_;
-    if (p_ >= e_ || !(*p_ >= '0' && *p_ <= '9')) return err("bad number");
-    while (p_ < e_ && ((*p_ >= '0' && *p_ <= '9') || *p_ == '.' || *p_ == 'e' || *p_ == 'E' ||
-                       *p_ == '+' || *p_ == '-'))
-      ++p_;
-    o.kind = JVal::NUM;
-    o.s.assign(b, p_);
+    while (p_ < e_ && literal_char(*p_)) ++p_;
+    if (p_ == b) return err("expected value");
+    o.assign(b, p_);
     return true;
+  }
+  static bool keyword(const std::string &s, const char *lower) {
+    const size_t n = std::strlen(lower);
+    if (s.size() != n) return false;
+    for (size_t i = 0; i < n; ++i)
+      if (s[i] != lower[i] && s[i] != lower[i] - 32) return false;
+    return true;
+  }
+  static bool json_number(const std::string &s) {  // -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?
+    size_t i = 0, n = s.size();
+    if (i < n && s[i] == '-') ++i;
+    if (i >= n) return false;
+    if (s[i] == '0') ++i;
+    else if (s[i] >= '1' && s[i] <= '9') while (i < n && s[i] >= '0' && s[i] <= '9') ++i;
+    else return false;
+    if (i < n && s[i] == '.') {
+      ++i;
+      if (i >= n || s[i] < '0' || s[i] > '9') return false;
+      while (i < n && s[i] >= '0' && s[i] <= '9') ++i;
+    }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+      ++i;
+      if (i < n && (s[i] == '+' || s[i] == '-')) ++i;
+      if (i >= n || s[i] < '0' || s[i] > '9') return false;
+      while (i < n && s[i] >= '0' && s[i] <= '9') ++i;
+    }
+    return i == n;
+  }
+  bool name(std::string &k) {
+    if (*p_ == '"' || *p_ == '\'') return string(k, *p_);
+    return unquoted(k);
   }
   bool value(JVal &o, int depth) {
     if (depth > 512) return err("nesting too deep");
-    ws();
+    if (!ws()) return false;
     if (p_ >= e_) return err("unexpected end");
     char c = *p_;
     if (c == '{') {
       ++p_;
       o.kind = JVal::OBJ;
-      ws();
+      if (!ws()) return false;
       if (p_ < e_ && *p_ == '}') { ++p_; return true; }
       while (true) {
-        ws();
-        if (p_ >= e_ || *p_ != '"') return err("expected key");
+        if (!ws()) return false;
+        if (p_ >= e_ || *p_ == '}') return err("expected name");
         std::string k;
-        if (!string(k)) return false;
-        ws();
-        if (p_ >= e_ || *p_ != ':') return err("expected ':'");
-        ++p_;
+        if (!name(k)) return false;
+        if (!ws()) return false;
+        if (p_ < e_ && *p_ == ':') ++p_;
+        else if (p_ < e_ && *p_ == '=') { ++p_; if (p_ < e_ && *p_ == '>') ++p_; }
+        else return err("expected ':'");
         JVal v;
         if (!value(v, depth + 1)) return false;
         o.obj.emplace_back(std::move(k), std::move(v));
-        ws();
-        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (!ws()) return false;
+        if (p_ < e_ && (*p_ == ',' || *p_ == ';')) { ++p_; continue; }
         if (p_ < e_ && *p_ == '}') { ++p_; return true; }
         return err("expected ',' or '}'");
       }
@@ -236,26 +293,42 @@ class JParser {
     if (c == '[') {
       ++p_;
       o.kind = JVal::ARR;
-      ws();
+      if (!ws()) return false;
       if (p_ < e_ && *p_ == ']') { ++p_; return true; }
       while (true) {
-        JVal v;
-        if (!value(v, depth + 1)) return false;
-        o.arr.push_back(std::move(v));
-        ws();
-        if (p_ < e_ && *p_ == ',') { ++p_; continue; }
+        if (!ws()) return false;
+        if (p_ < e_ && (*p_ == ',' || *p_ == ';' || *p_ == ']')) {
+          o.arr.emplace_back();  // an omitted element is null (lenient)
+        } else {
+          JVal v;
+          if (!value(v, depth + 1)) return false;
+          o.arr.push_back(std::move(v));
+        }
+        if (!ws()) return false;
+        if (p_ < e_ && (*p_ == ',' || *p_ == ';')) { ++p_; continue; }
         if (p_ < e_ && *p_ == ']') { ++p_; return true; }
         return err("expected ',' or ']'");
       }
     }
-    if (c == '"') {
+    if (c == '"' || c == '\'') {
       o.kind = JVal::STR;
-      return string(o.s);
+      return string(o.s, c);
     }
-    if (c == 't') { o.kind = JVal::BOOL; o.b = true; return lit("true"); }
-    if (c == 'f') { o.kind = JVal::BOOL; o.b = false; return lit("false"); }
-    if (c == 'n') { o.kind = JVal::NUL; return lit("null"); }
-    return number(o);
+    std::string lit;
+    if (!unquoted(lit)) return false;
+    if (keyword(lit, "true") || keyword(lit, "false")) {
+      o.kind = JVal::BOOL;
+      o.b = (lit[0] == 't' || lit[0] == 'T');
+    } else if (keyword(lit, "null")) {
+      o.kind = JVal::NUL;
+    } else if (json_number(lit)) {
+      o.kind = JVal::NUM;
+      o.s = lit;
+    } else {
+      o.kind = JVal::STR;
+      o.s = lit;
+    }
+    return true;
   }
 };
 

@@ -107,3 +107,44 @@ def test_native_edge_list_matches_python_reader(golden_cases):
         urls, src, dst = sparky_hip.read_edge_list(c["lines"])
         assert names == urls
         assert got == [(urls[s], None if d < 0 else urls[d]) for s, d in zip(src.tolist(), dst.tolist())]
+
+
+# Gson's lenient reader (Sparky.java:87 `new JsonParser().parse(String)`): records a strict
+# RFC 8259 parser would reject.  Native front-end against the oracle restatement; both restate
+# Gson's published lenient rules, and no reference run pins them (parity unpinned).
+LENIENT = [
+    "http://l1.com/\t{'content': {'links': [{'href': 'http://x.com/', 'type': 'a'}]}}",  # single quotes
+    "http://l2.com/\t{content: {links: [{href: y.com?q, type: a}]}}",  # unquoted names/strings (no : / in them)
+    "http://l3.com/\t{\"content\" = {\"links\" => [{\"href\": \"http://z.com/\"; \"type\": \"a\"}]}}",  # = => ;
+    "http://l4.com/\t{\"content\": {\"links\": [{\"href\": \"http://x.com/\", \"type\": \"a\"}], \"o\": [1,,2,]}}",  # nulls
+    "http://l5.com/\t// lead comment\n",  # placeholder replaced below (comments need one line)
+    "http://l6.com/\t{\"content\": {\"links\": [{\"href\": NaN, \"type\": a}, {\"href\": 01, \"type\": a},"
+    " {\"href\": -0, \"type\": a}, {\"href\": TRUE, \"type\": a}, {\"href\": nulL, \"type\": a}]}}",
+    "http://l7.com/\t)]}'\n",  # placeholder (prefix)
+]
+LENIENT[4] = "http://l5.com/\t/* c */ {\"content\": /* in */ {\"links\": []}} # trailing comment"
+LENIENT[6] = "http://l7.com/\t{\"content\": {\"links\": [{\"href\": \"u\\'q\", \"type\": 'a'}]}} /* tail */"
+
+
+def test_ccjson_lenient_records_match_oracle():
+    want = sparky_rdd.pairs_from_ccjson_lines(LENIENT)
+    got, _ = native("\n".join(LENIENT) + "\n")
+    assert got == want
+    d = {}
+    for u, v in want:
+        d.setdefault(u, []).append(v)
+    assert d["http://l1.com/"] == ["http://x.com/"] and d["http://l2.com/"] == ["y.com?q"]
+    assert d["http://l3.com/"] == ["http://z.com/"] and d["http://l4.com/"] == ["http://x.com/"]
+    assert d["http://l5.com/"] == [None]  # no links: a record without links
+    # unquoted NaN / 01 are strings, -0 a number, TRUE / nulL keywords (Gson's peekKeyword)
+    assert d["http://l6.com/"] == ["NaN", "01", "-0", "true", "null"]
+
+
+@pytest.mark.parametrize("bad", ["{\"content\": {\"a\": 1,}}", "{content: {links: [{href: http://x.com/}]}}", "{\"content\": 1} {\"x\": 2}", "{'a': 'open}",
+                                 "{/* unterminated : 1}", "{\"a\" 1}",
+                                 "{\"content\": {\"links\": [{\"href\": \"h\", \"type\": \"a\"},,]}}"])
+def test_ccjson_lenient_still_rejects(bad):
+    with pytest.raises(HostError):
+        native(f"http://bad.com/\t{bad}\n")
+    with pytest.raises(ValueError):
+        sparky_rdd.pairs_from_ccjson_lines([f"http://bad.com/\t{bad}"])
