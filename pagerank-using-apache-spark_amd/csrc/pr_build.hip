@@ -344,8 +344,10 @@ __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *_
   }
 }
 
-// One wave per unit: moves the end marks into the lane metadata word (end mask, the static
-// predicates of the segmented scan, the lane's first segment index) and clears them in the codes.
+// One wave per unit: the lane metadata word (end mask, the static predicates of the segmented
+// scan, the lane's first segment index) from the end marks in bit 0 of the codes, which stay
+// (the kernel masks them).  Only for PR_HOT_META=1: by default k_spmv_hot derives the same word
+// in-kernel (pr_spmv.h derive_meta).
 __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *__restrict__ units,
                                                   uint32_t *__restrict__ colh, uint32_t *__restrict__ meta) {
   const int t = threadIdx.x;
@@ -361,7 +363,6 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
       endm |= (e ? 1u : 0u) << j;
       const unsigned long long bm = __ballot(e);
       excl += __popcll(bm & lanemask_lt());
-      if (live) c[j] = v & ~1u;
     }
     const unsigned long long F = __ballot(endm != 0);
     // no segment end among lanes [lo, t]
@@ -675,7 +676,8 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
-    PR_TRY(g->hmeta.alloc(sizeof(uint32_t) * kWave * (nu + 1)));
+    if (const char *e = getenv("PR_HOT_META")) g->hot_meta = atoi(e) != 0;  // A/B knob
+    PR_TRY(g->hmeta.alloc(g->hot_meta ? sizeof(uint32_t) * kWave * (nu + 1) : 8));
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
     g->n_slots = poff[C];
@@ -686,8 +688,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
       hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
                          g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
                          hotidx.as<int32_t>(), g->colh.as<uint32_t>());
-      hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(kWave), 0, s, nu,
-                         g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
+      if (g->hot_meta)
+        hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(kWave), 0, s, nu,
+                           g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
       PR_HIP(hipGetLastError());
       PR_HIP(hipStreamSynchronize(s));
     }

@@ -249,11 +249,9 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   // runs of iteration k may still be pending when this part packs iteration k + 1
   PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
   PR_HIP(hipStreamSynchronize(s));
-  // chunks of the overlapped exchange: one per hot phase (PR_XCHG_CHUNKS=0: one chunk, i.e. the
-  // next iteration waits for the whole exchange -- the A/B reference)
+  // chunk bounds of the overlapped exchange: one chunk per hot phase (whether the chunks travel
+  // separately is decided when the transport is known: x_chunked, set_exchange_chunking)
   g->n_xc = (g->C > 1 && g->hot_phased) ? std::max(1, g->C / kXcds) : 1;
-  if (const char *e = getenv("PR_XCHG_CHUNKS"))
-    if (atoi(e) == 0) g->n_xc = 1;
   PR_TRY(chunk_bounds(g, g->x_send.as<uint32_t>(), g->x_soff, true, &g->x_sch));
   PR_TRY(chunk_bounds(g, recv.as<uint32_t>(), g->x_roff, false, &g->x_rch));
   PR_HIP(hipStreamCreateWithFlags(&g->xstream, hipStreamNonBlocking));
@@ -283,7 +281,9 @@ int verify_exchange(pr_graph *g) {
   mine[0] = g->V;
   mine[1] = g->S_pad;
   mine[2] = g->x_allgather ? 1 : 0;
-  mine[P + 3] = g->n_xc;  // chunking of the overlapped exchange (PR_XCHG_CHUNKS, PR_HOT_PHASED)
+  // chunking of the overlapped exchange (PR_XCHG_CHUNKS, PR_HOT_PHASED): the grouped send/recv
+  // calls of every chunk must pair up between the ranks
+  mine[P + 3] = 2 * (int64_t)g->n_xc + (g->x_chunked ? 1 : 0);
   if (!g->x_allgather)
     for (int q = 0; q < P; ++q) mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
   DevBuf d;
@@ -325,14 +325,15 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
   PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
   if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
-  const int nc = g->n_xc;
+  const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
   const double *sruns = send_runs(g, buf);
-  for (int c = 0; c < nc; ++c) {
+  for (int c = 0; c < steps; ++c) {
+    const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;  // unchunked: whole runs
     ncclResult_t rc = ncclGroupStart();
     for (int q = 0; q < g->nparts && rc == ncclSuccess; ++q) {
       if (q == g->part) continue;
-      const int64_t s0 = g->x_sch[(size_t)q * (nc + 1) + c], s1 = g->x_sch[(size_t)q * (nc + 1) + c + 1];
-      const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + c], r1 = g->x_rch[(size_t)q * (nc + 1) + c + 1];
+      const int64_t s0 = g->x_sch[(size_t)q * (nc + 1) + lo], s1 = g->x_sch[(size_t)q * (nc + 1) + hi];
+      const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
       // both ends derive the chunk sizes from the same positions: a zero-size pair is skipped on both
       if (s1 > s0) rc = ncclSend(sruns + g->x_soff[q] + s0, (size_t)(s1 - s0), ncclDouble, q, g->comm, g->xstream);
       if (rc == ncclSuccess && r1 > r0)
@@ -341,7 +342,7 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
     const ncclResult_t rc2 = ncclGroupEnd();
     if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(rc));
     if (rc2 != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclGroupEnd: ") + ncclGetErrorString(rc2));
-    PR_HIP(hipEventRecord(g->x_ev[c], g->xstream));
+    PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
   }
   if (ev_b) PR_HIP(hipEventRecord(ev_b, g->xstream));
   g->x_pending = true;
@@ -375,20 +376,21 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
       continue;
     }
     for (int p = 0; p < n; ++p) PR_HIP(hipStreamWaitEvent(g->xstream, parts[p]->x_pack_ev, 0));
-    const int nc = g->n_xc;
-    for (int c = 0; c < nc; ++c) {
+    const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
+    for (int c = 0; c < steps; ++c) {
+      const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;  // unchunked: whole runs
       for (int p = 0; p < n; ++p) {
         if (p == q) continue;
         const pr_graph *src = parts[p];
-        const int64_t r0 = g->x_rch[(size_t)p * (nc + 1) + c], r1 = g->x_rch[(size_t)p * (nc + 1) + c + 1];
-        const int64_t s0 = src->x_sch[(size_t)q * (nc + 1) + c], s1 = src->x_sch[(size_t)q * (nc + 1) + c + 1];
+        const int64_t r0 = g->x_rch[(size_t)p * (nc + 1) + lo], r1 = g->x_rch[(size_t)p * (nc + 1) + hi];
+        const int64_t s0 = src->x_sch[(size_t)q * (nc + 1) + lo], s1 = src->x_sch[(size_t)q * (nc + 1) + hi];
         if (r1 - r0 != s1 - s0) return fail(PR_ERR_STATE, "exchange lists disagree");
         if (r1 > r0)
           PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + g->S_pad + g->x_roff[p] + r0,
                                 send_runs(src, buf) + src->x_soff[q] + s0, sizeof(double) * (r1 - r0),
                                 hipMemcpyDeviceToDevice, g->xstream));
       }
-      PR_HIP(hipEventRecord(g->x_ev[c], g->xstream));
+      PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
     }
     g->x_pending = true;
   }

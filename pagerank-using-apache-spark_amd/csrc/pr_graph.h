@@ -67,6 +67,7 @@ struct pr_graph {
   pr::HotGeom hot{};
   int hot_grid = 0;  // workgroups of k_spmv_hot (a multiple of C: one per CU)
   bool hot_phased = false;  // an XCD's classes one after another (k_spmv_hot PHASED)
+  bool hot_meta = false;    // lane metadata precomputed in hmeta (PR_HOT_META=1) instead of derived in-kernel
   bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
   bool epi_grp = false;     // epi_abs + a sentinel cbase row: k_epilogue_grp (LDS-staged class runs)
   int epi_var = 0;          // its (group, window) variant, pr_spmv.h kEpiVariants (PR_EPI_VAR)
@@ -112,6 +113,9 @@ struct pr_graph {
   // the next iteration's phase c waits for x_ev[c] only (pr_iter.hip), so the transfer of the
   // later classes overlaps the SpMV of the earlier ones.
   int n_xc = 1;
+  // whether the chunks travel separately (set when the transport is known: RCCL attach, group
+  // reset); otherwise whole runs, and the next iteration waits for all of them
+  bool x_chunked = false;
   std::vector<int64_t> x_sch, x_rch;
   hipStream_t xstream = nullptr;
   std::vector<hipEvent_t> x_ev;
@@ -137,6 +141,10 @@ int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);
 int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange
+// x_chunked from PR_XCHG_CHUNKS (0: never, 1: always) or, unset, auto_on (RCCL: always; a
+// single-process group: when its parts span several GPUs -- on one GPU the copies and the
+// phase-split launches compete for the same device and the chunking only costs)
+void set_exchange_chunking(pr_graph *g, bool auto_on);
 int n_hot_phases(const pr_graph *g);
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur

@@ -156,10 +156,11 @@ int prepare_hot_kernel() {
     for (int c : {8, 16, 32, 64, 128})
       PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v)),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
-  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (const void *k : {reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1, false>)})
+    PR_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   return PR_OK;
 }
 
@@ -167,7 +168,8 @@ int n_hot_phases(const pr_graph *g) { return g->hot_phased ? std::max(1, g->C / 
 
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   const size_t lds = g->hot.lds_bytes();
-  auto *kern = g->hot_phased ? &k_spmv_hot<0, 0, 1> : &k_spmv_hot<0, 0, 0>;
+  auto *kern = g->hot_meta ? (g->hot_phased ? &k_spmv_hot<0, 0, 1, false> : &k_spmv_hot<0, 0, 0, false>)
+                           : (g->hot_phased ? &k_spmv_hot<0, 0, 1, true> : &k_spmv_hot<0, 0, 0, true>);
   if (ph1 < 0) ph1 = n_hot_phases(g);
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
@@ -176,6 +178,12 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
                      g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
+}
+
+void set_exchange_chunking(pr_graph *g, bool auto_on) {
+  bool on = auto_on;
+  if (const char *e = getenv("PR_XCHG_CHUNKS")) on = atoi(e) != 0;  // A/B knob
+  g->x_chunked = on && g->n_xc > 1;
 }
 
 int join_exchange(pr_graph *g) {
@@ -240,7 +248,7 @@ int iter_compute(pr_graph *g) {
   int64_t n_parts = g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
     const int nph = n_hot_phases(g);
-    if (g->n_hunits > 0 && g->x_pending && g->n_xc == nph && nph > 1) {
+    if (g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1) {
       // overlapped exchange: hot phase c needs only chunk c of the runs received from every peer
       for (int c = 0; c < nph; ++c) {
         PR_HIP(hipStreamWaitEvent(s, g->x_ev[c], 0));

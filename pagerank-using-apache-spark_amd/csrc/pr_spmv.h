@@ -282,9 +282,13 @@ __device__ __forceinline__ double dpp_f64(double x) {
 
 struct WaveCodes {
   uint32_t c[kWavePT];
-  uint32_t meta;
+  uint32_t meta;  // only with MIK = 0 (precomputed hmeta words)
 };
 
+// MIK (meta in kernel, the default): the lane metadata is derived from the segment-end marks
+// the codes carry in bit 0 (derive_meta) instead of a precomputed word per lane (hmeta,
+// 4 B per lane and unit: 0.53 GB per pass at R-MAT s26).
+template <bool MIK>
 __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *__restrict__ colh,
                                                 const uint32_t *__restrict__ hmeta, int64_t k, WaveCodes &w) {
   // per-unit descriptor: base and size are wave-uniform (u lives in SGPRs)
@@ -299,9 +303,53 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *_
     w.c[4 * q + 2] = (uint32_t)x.z;
     w.c[4 * q + 3] = (uint32_t)x.w;
   }
-  const __amdgpu_buffer_rsrc_t ms =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(hmeta + k * kWave), 0, u.n > 0 ? kWave * 4 : 0, 0x00020000);
-  w.meta = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ms, lane_id() * 4, 0, 2);
+  if constexpr (!MIK) {
+    const __amdgpu_buffer_rsrc_t ms =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(hmeta + k * kWave), 0, u.n > 0 ? kWave * 4 : 0, 0x00020000);
+    w.meta = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(ms, lane_id() * 4, 0, 2);
+  } else {
+    w.meta = 0;
+  }
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
+}
+
+// The lane metadata of a STREAM unit (pr_internal.h) from the end marks in bit 0 of its codes:
+// which of the lane's entries end a segment, the six "add the partner" predicates of the wave's
+// segmented scan (the partner lanes up to this one hold no segment end), and the index of the
+// lane's first segment end within the unit (an exclusive scan of the per-lane end counts).
+__device__ __forceinline__ uint32_t derive_meta(const WaveCodes &w) {
+  uint32_t endm = 0;
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) endm |= (w.c[j] & 1u) << j;
+  const int t = lane_id(), r = t & 15, row = t >> 4;
+  const uint64_t F = __ballot(endm != 0u);
+  const uint64_t upto = (t == 63) ? ~0ull : ((1ull << (t + 1)) - 1);  // lanes [0, t]
+  auto clear = [&](int lo) { return (F & upto & ~((1ull << lo) - 1)) == 0ull; };  // no end in [lo, t]
+  uint32_t cond = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 1 << s;
+    if (r >= k && clear(t - k + 1)) cond |= 1u << s;
+  }
+  if ((row == 1 || row == 3) && clear(row * 16)) cond |= 1u << 4;
+  if (row >= 2 && clear(32)) cond |= 1u << 5;
+  // inclusive wave scan of the end counts (row_shr 1/2/4/8, then row_bcast 15/31)
+  const int cnt = __builtin_popcount(endm);
+  int x = cnt;
+  x += dpp_i32<0x111>(x);
+  x += dpp_i32<0x112>(x);
+  x += dpp_i32<0x114>(x);
+  x += dpp_i32<0x118>(x);
+  int p = dpp_i32<0x142>(x);
+  if (row == 1 || row == 3) x += p;
+  p = dpp_i32<0x143>(x);
+  if (row >= 2) x += p;
+  const uint32_t excl = (uint32_t)(x - cnt);
+  return endm | (cond * kMetaStep0) | (excl << kMetaExclShift);
 }
 
 // DIAG (diagnostics library only; results wrong when != 0): 1 = every value from LDS (no
@@ -314,7 +362,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
                                                  double (&v)[kWavePT]) {
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) {
-    const uint32_t c = w.c[j];
+    const uint32_t c = w.c[j] & ~1u;  // bit 0: segment end mark (derive_meta)
     const bool glob = (int32_t)c < 0;
     uint32_t la = glob ? 0u : c;
     if constexpr (DIAG == 1 || DIAG == 13) la = c & 0xFFF8u;
@@ -338,7 +386,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
   }
 }
 
-template <int DIAG>
+template <int DIAG, bool MIK>
 __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
                                                  __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
                                                  double *stage) {
@@ -350,7 +398,8 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
-  const uint32_t endm = w.meta & 0xFFu;
+  const uint32_t meta = MIK ? derive_meta(w) : w.meta;
+  const uint32_t endm = meta & 0xFFu;
   double sv[kWavePT];
   double acc = 0.0;
 #pragma unroll
@@ -362,22 +411,22 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   // segmented inclusive scan of the lane tails; partner-add predicates precomputed
   double a = acc, p;
   p = dpp_f64<0x111>(a);  // row_shr:1
-  if (w.meta & kMetaStep0) a = __dadd_rn(p, a);
+  if (meta & kMetaStep0) a = __dadd_rn(p, a);
   p = dpp_f64<0x112>(a);  // row_shr:2
-  if (w.meta & (kMetaStep0 << 1)) a = __dadd_rn(p, a);
+  if (meta & (kMetaStep0 << 1)) a = __dadd_rn(p, a);
   p = dpp_f64<0x114>(a);  // row_shr:4
-  if (w.meta & (kMetaStep0 << 2)) a = __dadd_rn(p, a);
+  if (meta & (kMetaStep0 << 2)) a = __dadd_rn(p, a);
   p = dpp_f64<0x118>(a);  // row_shr:8
-  if (w.meta & (kMetaStep0 << 3)) a = __dadd_rn(p, a);
+  if (meta & (kMetaStep0 << 3)) a = __dadd_rn(p, a);
   p = dpp_f64<0x142>(a);  // row_bcast:15
-  if (w.meta & (kMetaStep0 << 4)) a = __dadd_rn(p, a);
+  if (meta & (kMetaStep0 << 4)) a = __dadd_rn(p, a);
   p = dpp_f64<0x143>(a);  // row_bcast:31
-  if (w.meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
+  if (meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
   const double carry = dpp_f64<0x138>(a);  // wave_shr:1 (lane 0 reads 0)
   // lane's first segment end gets the carry; segment s of the unit is row r0 + s.  The sums are
   // staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced 512-byte
   // stores instead of eight scattered store instructions.
-  const int e0 = (int)(w.meta >> kMetaExclShift), nseg = u.meta;
+  const int e0 = (int)(meta >> kMetaExclShift), nseg = u.meta;
   for (int base = 0; base < nseg; base += kStageSlots) {
     int e = e0 - base;
     bool first = true;
@@ -402,7 +451,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
 
 // One class's wave units, strided over `nteams` workgroups (this one is `team`), with the
 // class's hot set already in LDS.
-template <int ORDER, int DIAG>
+template <int ORDER, int DIAG, bool MIK>
 __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, const Unit *__restrict__ units,
                                                 const int64_t *__restrict__ ucum, const HotGeom &hg,
                                                 const uint32_t *__restrict__ colh,
@@ -429,9 +478,9 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   WaveCodes wc[3];
   double v[3][kWavePT];
   u[0] = unit_at(k);
-  wave_unit_codes(u[0], colh, hmeta, k, wc[0]);
+  wave_unit_codes<MIK>(u[0], colh, hmeta, k, wc[0]);
   u[1] = unit_at((k + stride < end) ? k + stride : none_k);
-  wave_unit_codes(u[1], colh, hmeta, k + stride, wc[1]);
+  wave_unit_codes<MIK>(u[1], colh, hmeta, k + stride, wc[1]);
   wave_unit_gather<DIAG>(wc[0], hot, crs, v[0]);
   while (true) {
 #pragma unroll
@@ -439,12 +488,12 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       const int s1 = (sl + 1) % 3, s2 = (sl + 2) % 3;
       const int64_t k2 = k + 2 * stride;
       u[s2] = unit_at(k2 < end ? k2 : none_k);
-      wave_unit_codes(u[s2], colh, hmeta, k2, wc[s2]);
+      wave_unit_codes<MIK>(u[s2], colh, hmeta, k2, wc[s2]);
       if constexpr (ORDER == 0) {
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
-        wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
       } else {  // reduce first: a gather issue stalled by a busy address unit cannot hold it up
-        wave_unit_reduce<DIAG>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
       }
       k += stride;
@@ -457,8 +506,9 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
 // puts workgroup b on XCD b % 8; XCD k owns classes k, k + 8, ...  PHASED = 0: the XCD's
 // workgroups are split between its classes, all running at once.  PHASED = 1: all of the XCD's
 // workgroups run its classes one after another, so its L2 holds one class's sources at a time
-// (1/C of the gather space instead of 8/C); the hot set is restaged per class.
-template <int ORDER = 0, int DIAG = 0, int PHASED = 0>
+// (1/C of the gather space instead of 8/C); the hot set is restaged per class.  MIK: lane
+// metadata derived in the kernel (default) or read from hmeta (A/B, PR_HOT_META=1).
+template <int ORDER = 0, int DIAG = 0, int PHASED = 0, bool MIK = true>
 __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
                                                           const int64_t *__restrict__ ucum, HotGeom hg,
                                                           const uint32_t *__restrict__ colh,
@@ -492,7 +542,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
     for (int i = threadIdx.x; i < nh; i += kHotThreads) hot[1 + i] = cin[hp[i]];
     if (threadIdx.x == 0) hot[0] = 0.0;
     __syncthreads();
-    hot_class_units<ORDER, DIAG>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,
+    hot_class_units<ORDER, DIAG, MIK>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,
                                  piece_part, stage, wv);
   }
 }

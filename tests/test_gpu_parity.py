@@ -473,7 +473,8 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
     phases and every peer's run travels in 8 chunks, chunk c = the positions of classes [8c, 8c+8);
     the next iteration's phase c waits only for chunk c.  Against the oracle, and bitwise equal to
     the same parts exchanging whole runs before the next iteration starts (PR_XCHG_CHUNKS=0): the
-    chunking moves the same values, only earlier."""
+    chunking moves the same values, only earlier.  PR_XCHG_CHUNKS=1 forces the chunking, which a
+    group whose parts share one GPU leaves off by default."""
     monkeypatch.setenv("PR_CLASSES", "64")
     monkeypatch.setenv("PR_HOT_SLOTS", "600")
     rng = np.random.default_rng(60 + P)
@@ -483,8 +484,7 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
     ref = oracle_c.run(csr, 9)
     out = {}
     for chunks in ("on", "off"):
-        if chunks == "off":
-            monkeypatch.setenv("PR_XCHG_CHUNKS", "0")
+        monkeypatch.setenv("PR_XCHG_CHUNKS", "1" if chunks == "on" else "0")
         parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split")
                  for p in range(P)]
         try:
@@ -500,3 +500,22 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
                 p.close()
     assert np.array_equal(out["on"], out["off"])
     assert max_rel(out["on"], ref["ranks"]) <= RANK_TOL
+
+
+def test_lane_metadata_in_kernel_equals_precomputed(hip, oracle_c, monkeypatch):
+    """k_spmv_hot derives each lane's segment metadata from the end marks in its codes
+    (pr_spmv.h derive_meta); PR_HOT_META=1 reads the same words precomputed at build (hmeta).
+    Same sums, bit for bit, and both equal the oracle."""
+    monkeypatch.setenv("PR_CLASSES", "16")
+    monkeypatch.setenv("PR_HOT_SLOTS", "500")
+    rng = np.random.default_rng(123)
+    V = 40000
+    src, dst = random_edges(rng, V, 500000, hub_frac=0.03)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PR_HOT_META", mode)
+        with hip.PageRankGraph(V, src, dst, layout="split", keep_canonical=False) as g:
+            out[mode], _ = g.run(8)
+    assert np.array_equal(out["0"], out["1"])
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
+    assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
