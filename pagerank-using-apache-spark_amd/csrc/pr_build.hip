@@ -284,8 +284,8 @@ int build_padded_cols(const UnitPlan &plan, const int32_t *col, int32_t *colp, h
 }
 
 // ---- split layout: entry codes (pr_internal.h, pr_spmv.h k_spmv_hot) -----------------------
-// Entry code (pr_internal.h); a segment end is marked in bit 0 until k_unit_meta moves it into
-// the lane metadata (codes are byte offsets / addresses, multiples of 8).
+// Entry code (pr_internal.h); a segment end is marked in bit 0 (codes are byte offsets /
+// addresses, multiples of 8), from which k_spmv_hot derives its lane metadata.
 // hpos[x * P*Kp + p*Kp + q] = gather position of row x*Q_pad + q of part p (0 when q >= q_load or
 // the part never reads it: the slot is then never addressed); hotidx[pos] = its LDS slot.
 __global__ void k_hot_tables(HotGeom hg, const int32_t *__restrict__ cmap, int32_t *__restrict__ hpos,
@@ -651,6 +651,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
+    if (const char *e = getenv("PR_HOT_ASSIGN")) hg.assign = std::min(2, std::max(0, atoi(e)));
     g->hot = hg;
     // hot-set gather positions per class, and the LDS slot of every hot gather position
     DevBuf hotidx;

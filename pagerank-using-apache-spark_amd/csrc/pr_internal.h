@@ -122,13 +122,14 @@ constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
 
 // ---- heavy rows: wave units with an LDS-resident hot set (pr_spmv.h k_spmv_hot) -------------
 // A wave unit is one wavefront's work: kWavePT in-link entries per lane, kWaveUnit entries in
-// all.  STREAM: whole (row, class) segments of consecutive heavy rows, every segment non-empty
-// (a row without class-x in-links gets one dummy entry that reads a zero); PIECE: kWaveUnit
-// entries of one long segment.  Entries are 32-bit codes:
+// all.  STREAM: whole (row, class) segments of consecutive rows (only non-empty (row, class)
+// pairs are segments); PIECE: kWaveUnit entries of one long segment.  Entries are 32-bit codes:
 //   bit 31 set    kEntGlobal | byte offset of the contribution in the gather space (< 2 GiB)
 //   bit 31 clear  LDS byte address of a hot-set slot; slot 0 (address 0) holds 0.0
-// Padding and dummy entries are 0 -- also what a range-checked load past the unit returns.
-// Per unit and lane, one metadata word:
+//   bit 0         set on the last entry of a segment (both kinds are multiples of 8 otherwise)
+// Padding entries are 0 -- also what a range-checked load past the unit returns.  k_spmv_hot
+// derives its lane metadata from the end marks (pr_spmv.h derive_meta); with PR_HOT_META=1 the
+// build precomputes it instead, one word per unit and lane (hmeta):
 //   bits 0-7   which of the lane's entries end a segment (STREAM)
 //   bits 8-13  the six partner-add predicates of the wave's segmented scan (pr_spmv.h)
 //   bits 14-23 segment index of the lane's first end within the unit
@@ -175,6 +176,10 @@ struct SlotPos {
 struct HotGeom {
   int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;
+  // k_spmv_hot unit -> wave mapping (PR_HOT_ASSIGN A/B): 0 = the XCD's waves interleaved over
+  // its class's units, 1 = one contiguous run of units per wave, 2 = one run per workgroup
+  // with its waves interleaved in it
+  int assign;
   __host__ __device__ int slots() const { return P * Kp + 1; }
   __host__ __device__ int stage_off() const { return (slots() + 1) & ~1; }  // 16-byte aligned
   __host__ __device__ size_t lds_bytes() const {

@@ -462,9 +462,23 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   const int64_t p0 = poff[x];
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)(partial + p0), 0, (uint32_t)((poff[x + 1] - p0) * 8), 0x00020000);
-  const int64_t beg = ucum[x], end = ucum[x + 1];
-  const int64_t stride = (int64_t)nteams * (kHotThreads / kWave);
-  int64_t k = beg + (int64_t)team * (kHotThreads / kWave) + wv;
+  const int64_t beg = ucum[x];
+  int64_t end = ucum[x + 1];
+  constexpr int kWaves = kHotThreads / kWave;
+  int64_t stride = (int64_t)nteams * kWaves;
+  int64_t k = beg + (int64_t)team * kWaves + wv;
+  if (hg.assign == 1) {  // a contiguous run of units per wave
+    const int64_t per = (end - beg + stride - 1) / stride;
+    k = beg + ((int64_t)team * kWaves + wv) * per;
+    end = k + per < end ? k + per : end;
+    stride = 1;
+  } else if (hg.assign == 2) {  // a contiguous run per workgroup, its waves interleaved
+    const int64_t per = (end - beg + nteams - 1) / nteams;
+    const int64_t t0 = beg + (int64_t)team * per;
+    end = t0 + per < end ? t0 + per : end;
+    k = t0 + wv;
+    stride = kWaves;
+  }
   if (k >= end) return;
   // unit descriptors through the scalar cache; index n_units (= ucum[kMaxClasses]) is an empty unit
   const __attribute__((address_space(4))) pr_v4i *cu = (const __attribute__((address_space(4))) pr_v4i *)units;
