@@ -13,15 +13,16 @@
 //   rowinfo uint32[R]         out-degree | kRowSink (in D) | kRowIndeg0 | kRowHole
 //   r       fp64[R]           ranks, updated in place
 //
-// Column classes (C = 16 by default once the whole gather space outgrows the L2s, else C = 1):
-// local rank j -> class x = j % C, row L = x*Q_pad + j/C (also its position in the slice).
-// Split layout (C > 1): every row's in-links are split by the class of their source; each
-// non-empty (row, class) pair is a segment with one slot of a class-dense partial array.  Class-x
-// wave units run on one XCD (two classes per XCD), whose L2 then caches only class-x sources, and
-// address either the gather space or the class's LDS hot set (the first Kp rows of every part's
-// class-x region; pr_internal.h HotGeom, positions from the hpos table).  k_epilogue adds a row's
-// segment sums in class order.  Fused layout (C = 1, small graphs): rowptr/colp CSR with
-// 256-thread units and the update fused into the same kernel (pr_spmv.h k_spmv_units).
+// Column classes (C = 8..64 once the whole gather space passes 4 MiB -- the fewest whose class
+// region fits 3/4 of one XCD's L2 -- else C = 1): local rank j -> class x = j % C, row
+// L = x*Q_pad + j/C (also its position in the slice).  Split layout (C > 1): every row's in-links
+// are split by the class of their source; each non-empty (row, class) pair is a segment with one
+// slot of a class-dense partial array.  Class-x wave units run on XCD x % 8, one class after
+// another (phased), so its L2 caches only class-x sources; they address either the gather space
+// or the class's LDS hot set (the first Kp rows of every part's class-x region; pr_internal.h
+// HotGeom, positions from the hpos table).  k_epilogue_grp adds a row's segment sums in class
+// order.  Fused layout (C = 1, small graphs): rowptr/colp CSR with 256-thread units and the
+// update fused into the same kernel (pr_spmv.h k_spmv_units).
 #pragma once
 
 #include <rccl/rccl.h>
@@ -119,10 +120,8 @@ struct pr_graph {
   std::vector<int64_t> x_sch, x_rch;
   hipStream_t xstream = nullptr;
   std::vector<hipEvent_t> x_ev;
-  hipEvent_t x_pack_ev = nullptr, x_t0 = nullptr, x_t1 = nullptr;
+  hipEvent_t x_pack_ev = nullptr;
   bool x_pending = false;
-  int x_timed = 0;  // exchanges timed on xstream (x_t0 -> x_t1 of the last one)
-  double x_ms_sum = 0.0;
 
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
