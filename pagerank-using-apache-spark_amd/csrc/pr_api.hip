@@ -319,7 +319,7 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
   }
   g->comm_rank = rank;
   g->comm_size = n_ranks;
-  pr::set_exchange_chunking(g, true);  // one GPU per rank: chunks overlap the next iteration
+  pr::set_exchange_chunking(g);
   if (n_ranks > 1) {
     const int rv = pr::verify_exchange(g);
     if (rv != PR_OK) {
@@ -363,9 +363,7 @@ int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, dou
     g->grouped = true;
     g->teleport = teleport;
     g->damping = damping;
-    bool multi_device = false;
-    for (int32_t q = 0; q < n_parts; ++q) multi_device = multi_device || parts[q]->device != g->device;
-    pr::set_exchange_chunking(g, multi_device);
+    pr::set_exchange_chunking(g);
     PR_TRY(pr::iter_reset(g, init_ranks));
   }
   PR_TRY(pr::group_exchange(parts, n_parts, 0));

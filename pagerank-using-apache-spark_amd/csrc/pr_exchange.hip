@@ -270,22 +270,29 @@ int exchange_pack(pr_graph *g, int buf) {
   return PR_OK;
 }
 
-// After ncclCommInitRank: every rank publishes {graph shape, exchange mode, its send-run lengths}
-// and checks that what each peer sends it is exactly what it expects to receive, so a mismatch
-// (different inputs, different PR_EXCHANGE per rank) fails loudly at attach time instead of
-// desynchronising the send/receive pairs.
+// After ncclCommInitRank: every rank publishes {graph shape, exchange mode, its send-run lengths,
+// their chunk sizes} and checks that what each peer sends it is exactly what it expects to
+// receive, chunk by chunk, so a mismatch (different inputs, different PR_EXCHANGE /
+// PR_XCHG_CHUNKS / PR_HOT_PHASED per rank) fails loudly at attach time instead of desynchronising
+// the send/receive pairs.  The record has the same length on every rank (kMaxChunks slots per peer).
 int verify_exchange(pr_graph *g) {
-  const int P = g->nparts;
-  const int W = P + 4;
+  constexpr int kMaxChunks = kMaxClasses / kXcds;
+  const int P = g->nparts, nc = g->n_xc;
+  if (nc > kMaxChunks) return fail(PR_ERR_INVALID, "too many exchange chunks");
+  const int CH = P + 4;  // chunk sizes start here: [CH + q * kMaxChunks + c]
+  const int W = CH + P * kMaxChunks;
   std::vector<int64_t> mine(W, 0);
   mine[0] = g->V;
   mine[1] = g->S_pad;
   mine[2] = g->x_allgather ? 1 : 0;
-  // chunking of the overlapped exchange (PR_XCHG_CHUNKS, PR_HOT_PHASED): the grouped send/recv
-  // calls of every chunk must pair up between the ranks
-  mine[P + 3] = 2 * (int64_t)g->n_xc + (g->x_chunked ? 1 : 0);
+  // chunking of the overlapped exchange: the grouped send/recv calls of every chunk must pair up
+  mine[P + 3] = 2 * (int64_t)nc + (g->x_chunked ? 1 : 0);
   if (!g->x_allgather)
-    for (int q = 0; q < P; ++q) mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
+    for (int q = 0; q < P; ++q) {
+      mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
+      for (int c = 0; c < nc; ++c)
+        mine[CH + q * kMaxChunks + c] = g->x_sch[(size_t)q * (nc + 1) + c + 1] - g->x_sch[(size_t)q * (nc + 1) + c];
+    }
   DevBuf d;
   PR_TRY(d.alloc(sizeof(int64_t) * (size_t)W * (P + 1)));
   PR_HIP(hipMemcpyAsync(d.as<int64_t>(), mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, g->stream));
@@ -294,13 +301,17 @@ int verify_exchange(pr_graph *g) {
   std::vector<int64_t> all((size_t)W * P);
   PR_HIP(hipMemcpyAsync(all.data(), d.as<int64_t>() + W, sizeof(int64_t) * W * P, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
+  const int me = g->part;
   for (int q = 0; q < P; ++q) {
     const int64_t *o = all.data() + (size_t)q * W;
     if (o[0] != g->V || o[1] != g->S_pad) return fail(PR_ERR_INVALID, "ranks hold parts of different graphs");
     if (o[2] != mine[2]) return fail(PR_ERR_INVALID, "ranks disagree on PR_EXCHANGE");
     if (o[P + 3] != mine[P + 3]) return fail(PR_ERR_INVALID, "ranks disagree on the exchange chunking");
-    if (q != g->part && !g->x_allgather && o[3 + g->part] != g->x_roff[q + 1] - g->x_roff[q])
-      return fail(PR_ERR_STATE, "exchange lists disagree between ranks");
+    if (q == me || g->x_allgather) continue;
+    if (o[3 + me] != g->x_roff[q + 1] - g->x_roff[q]) return fail(PR_ERR_STATE, "exchange lists disagree between ranks");
+    for (int c = 0; c < nc; ++c)
+      if (o[CH + me * kMaxChunks + c] != g->x_rch[(size_t)q * (nc + 1) + c + 1] - g->x_rch[(size_t)q * (nc + 1) + c])
+        return fail(PR_ERR_STATE, "exchange chunks disagree between ranks");
   }
   return PR_OK;
 }

@@ -114,8 +114,8 @@ struct pr_graph {
   // the next iteration's phase c waits for x_ev[c] only (pr_iter.hip), so the transfer of the
   // later classes overlaps the SpMV of the earlier ones.
   int n_xc = 1;
-  // whether the chunks travel separately (set when the transport is known: RCCL attach, group
-  // reset); otherwise whole runs, and the next iteration waits for all of them
+  // whether the chunks travel separately (PR_XCHG_CHUNKS=1, set at RCCL attach / group reset);
+  // otherwise whole runs, and the next iteration waits for all of them
   bool x_chunked = false;
   std::vector<int64_t> x_sch, x_rch;
   hipStream_t xstream = nullptr;
@@ -140,10 +140,11 @@ int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);
 int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange
-// x_chunked from PR_XCHG_CHUNKS (0: never, 1: always) or, unset, auto_on (RCCL: always; a
-// single-process group: when its parts span several GPUs -- on one GPU the copies and the
-// phase-split launches compete for the same device and the chunking only costs)
-void set_exchange_chunking(pr_graph *g, bool auto_on);
+// x_chunked from PR_XCHG_CHUNKS (1: the overlapped exchange; unset or 0: whole runs, the next
+// iteration waits for all of them).  Off by default: the transfers are kernels (RCCL, blit
+// copies) that compete with k_spmv_hot for CUs -- k_spmv_hot takes a CU's whole LDS, so the two
+// cannot share one -- and on one GPU the chunked group ran 8 % slower.
+void set_exchange_chunking(pr_graph *g);
 int n_hot_phases(const pr_graph *g);
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur

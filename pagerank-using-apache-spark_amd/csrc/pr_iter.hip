@@ -180,9 +180,9 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   return PR_OK;
 }
 
-void set_exchange_chunking(pr_graph *g, bool auto_on) {
-  bool on = auto_on;
-  if (const char *e = getenv("PR_XCHG_CHUNKS")) on = atoi(e) != 0;  // A/B knob
+void set_exchange_chunking(pr_graph *g) {
+  bool on = false;
+  if (const char *e = getenv("PR_XCHG_CHUNKS")) on = atoi(e) != 0;
   g->x_chunked = on && g->n_xc > 1;
 }
 
