@@ -2,7 +2,7 @@
 //
 //   pagerank <input-path> [iterations=10] [--format=edges|ccjson] [--out DIR]
 //            [--save-every-iter] [--dangling=local|none] [--device N] [--quiet] [--stats]
-//            [--resume DIR/PageRank<i>]
+//            [--resume DIR/PageRank<i>] [--devices D0,D1,...]
 //
 // Input (libpagerank_host): "src dst" edge list ("src" alone = record without links), or
 // --format=ccjson "url<TAB>json" Common Crawl metadata records (Sparky.java:61-123).  URLs are
@@ -15,6 +15,10 @@
 // instead of 1.0 (Sparky.java:165-170) and continue the same loop: iterations i+1 .. N-1, with
 // the same "Starting iter" lines and PageRank<iter> numbering.  A directory not named
 // PageRank<i> starts the loop at 0.
+// --devices D0,D1,...: one row part per listed GPU (a device may repeat), driven from this one
+// process by the pr_group_* API; the parts exchange contributions by device copies (xGMI peer
+// copies between GPUs).  Same outputs as one GPU.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -32,14 +36,29 @@ struct Options {
   bool save_every = false, quiet = false, stats = false;
   uint32_t flags = PR_DANGLING_LOCAL;
   int device = 0;
+  std::vector<int> devices;  // --devices: one part per entry (empty: one part on `device`)
 };
+
+std::vector<int> parse_devices(const std::string &s) {
+  std::vector<int> d;
+  size_t i = 0;
+  while (i <= s.size()) {
+    const size_t j = s.find(',', i);
+    const std::string t = s.substr(i, j == std::string::npos ? std::string::npos : j - i);
+    if (t.empty() || t.find_first_not_of("0123456789") != std::string::npos) return {};
+    d.push_back(std::atoi(t.c_str()));
+    if (j == std::string::npos) break;
+    i = j + 1;
+  }
+  return d;
+}
 
 [[noreturn]] void usage(const char *msg) {
   if (msg) std::fprintf(stderr, "pagerank: %s\n", msg);
   std::fprintf(stderr,
                "usage: pagerank <input-path> [iterations=10] [--format=edges|ccjson] [--out DIR]\n"
                "                [--save-every-iter] [--dangling=local|none] [--device N] [--quiet] [--stats]\n"
-               "                [--resume DIR/PageRank<i>]\n");
+               "                [--resume DIR/PageRank<i>] [--devices D0,D1,...]\n");
   std::exit(2);
 }
 
@@ -60,6 +79,10 @@ Options parse(int argc, char **argv) {
     else if (a == "--device" && i + 1 < argc) o.device = std::atoi(argv[++i]);
     else if (a == "--resume" && i + 1 < argc) o.resume = argv[++i];
     else if (a.rfind("--resume=", 0) == 0) o.resume = a.substr(9);
+    else if ((a == "--devices" && i + 1 < argc) || a.rfind("--devices=", 0) == 0) {
+      o.devices = parse_devices(a == "--devices" ? std::string(argv[++i]) : a.substr(10));
+      if (o.devices.empty()) usage("--devices takes a comma-separated list of device numbers");
+    }
     else if (a == "-h" || a == "--help") usage(nullptr);
     else if (!a.empty() && a[0] == '-') usage(("unknown option " + a).c_str());
     else if (pos == 0) { o.path = a; ++pos; }
@@ -104,6 +127,38 @@ void on_iter(int32_t it_run, const double *ranks, double dc, double l1, double m
   if (it + 1 < o.iterations) std::printf("Starting iter%d\n", it + 1);
 }
 
+// --devices: build one part per device, then run the iterations as a single-process group with
+// the same callback protocol as pr_run (ranks merged from every part, dc / L1 from part 0's
+// stats, which sum every part's slots).
+int run_group(const Options &o, const prh_edges *edges, const double *init, int n_run, Job *job,
+              std::vector<double> *ranks) {
+  const int P = (int)o.devices.size();
+  const int32_t V = prh_n_vertices(edges);
+  std::vector<pr_graph *> parts(P, nullptr);
+  int rc = PR_OK;
+  for (int p = 0; p < P && rc == PR_OK; ++p)
+    rc = pr_graph_create_part(o.devices[p], p, P, V, prh_n_edges(edges), prh_src(edges), prh_dst(edges),
+                              o.flags | PR_NO_CANONICAL, &parts[p]);
+  const bool want = !o.out.empty();
+  if (rc == PR_OK) rc = pr_group_reset(parts.data(), P, 0.15, 0.85, init);
+  for (int it = 0; it < n_run && rc == PR_OK; ++it) {
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = pr_group_step(parts.data(), P, 1);
+    if (rc == PR_OK) rc = pr_group_sync(parts.data(), P);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    double st[PR_STAT_COUNT] = {0};
+    if (rc == PR_OK) rc = pr_get_stats(parts[0], st, PR_STAT_COUNT);
+    for (int p = 0; p < P && rc == PR_OK && want; ++p) rc = pr_get_ranks(parts[p], ranks->data());
+    if (rc == PR_OK) on_iter(it, want ? ranks->data() : nullptr, st[PR_STAT_LAST_DC], st[PR_STAT_LAST_L1], ms, job);
+  }
+  for (int p = 0; p < P && rc == PR_OK; ++p) rc = pr_get_ranks(parts[p], ranks->data());
+  const std::string err = rc == PR_OK ? std::string() : std::string(pr_last_error());
+  for (pr_graph *g : parts)
+    if (g) pr_graph_destroy(g);
+  if (rc != PR_OK) std::fprintf(stderr, "pagerank: multi-GPU run failed (%d): %s\n", rc, err.c_str());
+  return rc;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -114,35 +169,42 @@ int main(int argc, char **argv) {
     return 1;
   }
   const int32_t V = prh_n_vertices(edges);
-  pr_graph *g = nullptr;
-  int rc = pr_graph_create(o.device, V, prh_n_edges(edges), prh_src(edges), prh_dst(edges),
-                           o.flags | PR_NO_CANONICAL, &g);
-  if (rc != PR_OK) {
-    std::fprintf(stderr, "pagerank: graph build failed (%d): %s\n", rc, pr_last_error());
-    prh_free(edges);
-    return 1;
-  }
   Job job{&o, edges};
   std::vector<double> ranks((size_t)V + 1), init;
   if (!o.resume.empty()) {
     init.assign((size_t)V + 1, 0.0);
     if (prh_read_ranks(edges, o.resume.c_str(), init.data()) != 0) {
       std::fprintf(stderr, "pagerank: --resume: %s\n", prh_last_error());
-      pr_graph_destroy(g);
       prh_free(edges);
       return 1;
     }
     job.start = saved_iteration(o.resume) + 1;  // 0 when the directory is not PageRank<i>
   }
   const int n_run = o.iterations > job.start ? o.iterations - job.start : 0;
-  if (n_run > 0) std::printf("Starting iter%d\n", job.start);
-  rc = pr_run(g, n_run, 0.15, 0.85, init.empty() ? nullptr : init.data(), ranks.data(), on_iter,
-              o.out.empty() ? 0u : PR_CB_RANKS, &job);
-  pr_graph_destroy(g);
-  if (rc != PR_OK) {
-    std::fprintf(stderr, "pagerank: run failed (%d): %s\n", rc, pr_last_error());
-    prh_free(edges);
-    return 1;
+  const double *init_p = init.empty() ? nullptr : init.data();
+  if (o.devices.size() > 1) {
+    if (n_run > 0) std::printf("Starting iter%d\n", job.start);
+    if (run_group(o, edges, init_p, n_run, &job, &ranks) != PR_OK) {
+      prh_free(edges);
+      return 1;
+    }
+  } else {
+    const int dev = o.devices.empty() ? o.device : o.devices[0];
+    pr_graph *g = nullptr;
+    int rc = pr_graph_create(dev, V, prh_n_edges(edges), prh_src(edges), prh_dst(edges), o.flags | PR_NO_CANONICAL, &g);
+    if (rc != PR_OK) {
+      std::fprintf(stderr, "pagerank: graph build failed (%d): %s\n", rc, pr_last_error());
+      prh_free(edges);
+      return 1;
+    }
+    if (n_run > 0) std::printf("Starting iter%d\n", job.start);
+    rc = pr_run(g, n_run, 0.15, 0.85, init_p, ranks.data(), on_iter, o.out.empty() ? 0u : PR_CB_RANKS, &job);
+    pr_graph_destroy(g);
+    if (rc != PR_OK) {
+      std::fprintf(stderr, "pagerank: run failed (%d): %s\n", rc, pr_last_error());
+      prh_free(edges);
+      return 1;
+    }
   }
   std::fflush(stdout);
   if (!o.quiet && prh_write_has_rank(edges, nullptr, ranks.data()) != 0) {

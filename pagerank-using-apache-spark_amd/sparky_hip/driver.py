@@ -27,7 +27,7 @@ from typing import Dict, Iterable, List, Sequence, TextIO, Tuple
 
 import numpy as np
 
-from .graph import PageRankGraph
+from .graph import PageRankGraph, PartGroup
 
 
 def java_double_to_string(x: float) -> str:
@@ -133,6 +133,27 @@ def saved_iteration(path: str) -> int:
     return -1
 
 
+def _run_group(edges, devices, dangling, n_run, init, cb, want_ranks):
+    """--devices: one part per listed device, one process (pr_group_*); the callback gets the
+    merged ranks of every part after each iteration, as with PageRankGraph.run."""
+    P = len(devices)
+    parts = []
+    try:
+        for p, d in enumerate(devices):
+            parts.append(PageRankGraph(edges.n_vertices, edges.src, edges.dst, device=d, dangling=dangling,
+                                       keep_canonical=False, part=p, n_parts=P))
+        grp = PartGroup(parts)
+        grp.reset(init_ranks=init)
+        for it in range(n_run):
+            grp.step(1)
+            grp.sync()
+            cb(it, grp.ranks() if want_ranks else None, None)
+        return grp.ranks()
+    finally:
+        for g in parts:
+            g.close()
+
+
 def main(argv=None) -> int:
     from ._host import HostEdges
 
@@ -146,7 +167,15 @@ def main(argv=None) -> int:
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--quiet", action="store_true", help="omit the '<url> has rank' lines")
     ap.add_argument("--resume", default=None, metavar="DIR", help="start from saved (url,rank) part files")
+    ap.add_argument("--devices", default=None, metavar="D0,D1,...",
+                    help="one row part per listed GPU (a device may repeat), one process (pr_group_*)")
     a = ap.parse_args(argv)
+    devices = [a.device]
+    if a.devices is not None:
+        try:
+            devices = [int(t) for t in a.devices.split(",")]
+        except ValueError:
+            ap.error("--devices takes a comma-separated list of device numbers")
     edges = HostEdges.read(a.edge_list, a.format)  # native front-end + first-appearance interning
     out = sys.stdout
     init, start = None, 0
@@ -154,20 +183,23 @@ def main(argv=None) -> int:
         init = edges.read_ranks(a.resume)
         start = saved_iteration(a.resume) + 1
     n_run = max(a.iterations - start, 0)
-    with PageRankGraph(edges.n_vertices, edges.src, edges.dst, device=a.device, dangling=a.dangling,
-                       keep_canonical=False) as g:
-        # Sparky prints "Starting iter<i>" before each iteration (Sparky.java:188); the library
-        # calls back after iteration i, so the host prints the next line there.
-        def cb(it_run, ranks, _st):
-            it = start + it_run
-            if a.out and (a.save_every_iter or it == a.iterations - 1):
-                edges.write_part(a.out, it, ranks)
-            if it + 1 < a.iterations:
-                out.write(f"Starting iter{it + 1}\n")
+    # Sparky prints "Starting iter<i>" before each iteration (Sparky.java:188); the library
+    # calls back after iteration i, so the host prints the next line there.
+    def cb(it_run, ranks, _st):
+        it = start + it_run
+        if a.out and (a.save_every_iter or it == a.iterations - 1):
+            edges.write_part(a.out, it, ranks)
+        if it + 1 < a.iterations:
+            out.write(f"Starting iter{it + 1}\n")
 
-        if n_run > 0:
-            out.write(f"Starting iter{start}\n")
-        ranks, _ = g.run(n_run, callback=cb, want_ranks_in_callback=bool(a.out), init_ranks=init)
+    if n_run > 0:
+        out.write(f"Starting iter{start}\n")
+    if len(devices) == 1:
+        with PageRankGraph(edges.n_vertices, edges.src, edges.dst, device=devices[0], dangling=a.dangling,
+                           keep_canonical=False) as g:
+            ranks, _ = g.run(n_run, callback=cb, want_ranks_in_callback=bool(a.out), init_ranks=init)
+    else:
+        ranks = _run_group(edges, devices, a.dangling, n_run, init, cb, bool(a.out))
     out.flush()
     if not a.quiet:
         edges.write_has_rank(None, ranks)

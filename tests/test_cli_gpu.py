@@ -142,3 +142,49 @@ def test_cli_unwritable_out_fails(tmp_path, runner):
     res = subprocess.run(base + [str(inp), "3", "--out", str(blocker / "out")], capture_output=True, text=True,
                          env=env, timeout=120)
     assert res.returncode != 0
+
+
+@pytest.mark.parametrize("runner", ["cpp", "python"])
+def test_cli_devices_group(tmp_path, runner, oracle_c):
+    """--devices 0,0,0: three row parts driven as one group (pr_group_*; on a multi-GPU box each
+    entry is its own GPU) produce the same outputs as one part -- Starting iter lines, every
+    saved PageRank<i>, the has-rank lines -- within the oracle bar, also when resumed."""
+    rng = np.random.default_rng(21)
+    lines = [f"u{int(s)} u{int(d)}" for s, d in zip(rng.integers(0, 600, 5000), rng.integers(0, 700, 5000))]
+    lines += [f"u{i}" for i in range(600, 630)]  # records without links
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(lines) + "\n")
+    env = dict(os.environ, PYTHONPATH=PKG_DIR)
+    base = [CLI] if runner == "cpp" else [sys.executable, "-m", "sparky_hip"]
+    out = tmp_path / "grp"
+    res = subprocess.run(base + [str(inp), "6", "--out", str(out), "--save-every-iter", "--devices", "0,0,0"],
+                         capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert [ln for ln in res.stdout.splitlines() if ln.startswith("Starting")] == [f"Starting iter{i}" for i in range(6)]
+    from sparky_hip import read_edge_list
+
+    urls, src, dst = read_edge_list(lines)
+    csr = oracle_c.build_csr(len(urls), src, dst)
+    for it in range(6):
+        ref = oracle_c.run(csr, it + 1)["ranks"]
+        got = parse_part(out / f"PageRank{it}" / "part-00000")
+        assert max(abs(got[u] - ref[i]) / ref[i] for i, u in enumerate(urls)) <= 1e-9
+    final = parse_has_rank(res.stdout)
+    ref = oracle_c.run(csr, 6)["ranks"]
+    assert max(abs(final[u] - ref[i]) / ref[i] for i, u in enumerate(urls)) <= 1e-9
+    # resumed on two parts from the group's own save
+    cont = tmp_path / "cont"
+    r2 = subprocess.run(base + [str(inp), "6", "--out", str(cont), "--quiet", "--devices", "0,0",
+                                "--resume", str(out / "PageRank3")], capture_output=True, text=True, env=env, timeout=120)
+    assert r2.returncode == 0, r2.stderr
+    assert r2.stdout.splitlines() == ["Starting iter4", "Starting iter5"]
+    a5, b5 = parse_part(cont / "PageRank5" / "part-00000"), parse_part(out / "PageRank5" / "part-00000")
+    assert a5.keys() == b5.keys() and max(abs(a5[u] - b5[u]) / b5[u] for u in a5) <= 1e-13
+
+
+def test_cli_devices_rejects_bad_list(tmp_path):
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(KAT) + "\n")
+    for bad in ["", "0,,1", "a", "0,-1"]:
+        res = subprocess.run([CLI, str(inp), "3", "--devices", bad], capture_output=True, text=True, timeout=60)
+        assert res.returncode == 2 and "--devices" in res.stderr
