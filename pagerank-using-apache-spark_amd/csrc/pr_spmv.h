@@ -551,9 +551,27 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
       team = (int)(blockIdx.x / hg.C);
       nteams = (int)(gridDim.x / hg.C);
     }
-    // stage the class's hot contributions (the previous iteration's, final before this launch)
+    // stage the class's hot contributions (the previous iteration's, final before this launch):
+    // every position load, then every gather in flight before the first LDS write -- a rolled
+    // loop pays two dependent memory latencies per element, 18 times per phase
     const int32_t *hp = hpos + (int64_t)x * nh;
-    for (int i = threadIdx.x; i < nh; i += kHotThreads) hot[1 + i] = cin[hp[i]];
+    constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18430 slots)
+    for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
+      int32_t pos[kSB];
+      double val[kSB];
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) {
+        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+        pos[j] = i < nh ? hp[i] : -1;
+      }
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) val[j] = pos[j] >= 0 ? cin[pos[j]] : 0.0;
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) {
+        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+        if (i < nh) hot[1 + i] = val[j];
+      }
+    }
     if (threadIdx.x == 0) hot[0] = 0.0;
     __syncthreads();
     hot_class_units<ORDER, DIAG, MIK>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,

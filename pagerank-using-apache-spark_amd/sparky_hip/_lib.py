@@ -12,7 +12,8 @@ import sys
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(os.path.dirname(_PKG_DIR), "build")
-LIB_PATH = os.path.join(BUILD_DIR, "libpagerank_hip.so")
+# PR_LIB_PATH: another build of the same library (A/B of two kernel versions on one box)
+LIB_PATH = os.environ.get("PR_LIB_PATH") or os.path.join(BUILD_DIR, "libpagerank_hip.so")
 
 PR_OK = 0
 PR_ERR_INVALID = -1
