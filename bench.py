@@ -17,7 +17,10 @@ Rank 0 prints ONE JSON line (the driver's contract), including
                   host's cores (N = 1 only): the median of iterations 2..K of the same graph;
   parity_max_rel: after the timed region, K iterations from a fresh reset on the GPU (every
                   rank's rows summed into one vector on rank 0 when N > 1) against K iterations
-                  of the oracle on the exported canonical CSR -- the north-star 1e-9 bar.
+                  of the oracle on the exported canonical CSR -- the north-star 1e-9 bar;
+  exchange_overlap_ab (N > 1): the K timed steps again with the exchange overlapped with the
+                  next iteration's SpMV phases (pr_set_option), beside the default's time; the
+                  parity leg then checks that mode too.
 """
 from __future__ import annotations
 
@@ -121,6 +124,8 @@ def main() -> int:
                     help="graph layout (A/B; auto picks by gather-space size)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (no cpu_baseline, no parity)")
     ap.add_argument("--parity-iters", type=int, default=10, help="K of the parity / cpu_baseline leg (Sparky.java:187)")
+    ap.add_argument("--no-overlap-ab", action="store_true",
+                    help="N > 1: skip the extra timed run with the exchange overlapped (pr_set_option)")
     a = ap.parse_args()
 
     import numpy as np
@@ -195,6 +200,29 @@ def main() -> int:
         dist.all_gather(allx, xt)
         xchg_ms = [float(x.item()) for x in allx]
 
+    # N > 1: the same K steps again with the exchange overlapped (one chunk per SpMV phase,
+    # pr_set_option, collective), reported beside the default; the parity leg checks both modes
+    overlap = None
+    if dist is not None and info.get("classes", 1) >= 16 and not a.no_overlap_ab:
+        g.set_exchange_chunks(True)
+        g.reset()
+        g.step(a.warmup)
+        g.sync()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.step(a.steps)
+        g.sync()
+        torch.cuda.synchronize()
+        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.barrier()
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        g.set_exchange_chunks(False)
+        overlap = {"unchunked_ms_per_step": round(ms_step, 4),
+                   "chunked_ms_per_step": round(float(tc.item()) / max(a.steps, 1) * 1e3, 4),
+                   "default": "unchunked", "chunks": info.get("classes", 1) // 8}
+        log(f"exchange overlap A/B: {overlap}")
+
     # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot per column class,
     # k_seg_reduce for long segments, k_epilogue_grp over all rows) -- on this rank
     spmv_ms = st["spmv_ms_mean"]
@@ -205,21 +233,33 @@ def main() -> int:
     cpu, parity = None, None
     if validate:
         K = a.parity_iters
-        g.reset()
-        g.step(K)
-        g.sync()
-        mine = np.zeros(V, np.float64)
-        g.ranks(mine)  # this rank's rows; the others stay 0
-        owned_once = True
-        if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
-            rt = torch.from_numpy(mine).cuda()
-            own = torch.from_numpy((mine != 0).astype(np.int32)).cuda()
-            dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
-            dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
-            if rank == 0:
-                mine = rt.cpu().numpy()
-                owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
-            del rt, own
+
+        def gpu_ranks():
+            """K iterations from a fresh reset; every rank's rows summed on rank 0."""
+            g.reset()
+            g.step(K)
+            g.sync()
+            mine = np.zeros(V, np.float64)
+            g.ranks(mine)  # this rank's rows; the others stay 0
+            owned_once = True
+            if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
+                rt = torch.from_numpy(mine).cuda()
+                own = torch.from_numpy((mine != 0).astype(np.int32)).cuda()
+                dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
+                dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
+                if rank == 0:
+                    mine = rt.cpu().numpy()
+                    owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
+                del rt, own
+            return mine, owned_once
+
+        mine, owned_once = gpu_ranks()
+        mine_chunked = None
+        if overlap is not None:
+            g.set_exchange_chunks(True)
+            mine_chunked, oc = gpu_ranks()
+            owned_once = owned_once and oc
+            g.set_exchange_chunks(False)
         if rank == 0:
             try:
                 res, threads, desc, e_csr = oracle_leg(g, V, K, pick_threads=(world == 1))
@@ -227,6 +267,9 @@ def main() -> int:
                 parity = {"iterations": K, "max_rel": float(np.max(np.abs(mine - ref) / ref)) if V else 0.0,
                           "vs": "oracle/pagerank_oracle.c on the exported canonical CSR",
                           "ranks_from": f"{world} rank(s)", "every_row_owned_once": owned_once}
+                if mine_chunked is not None:
+                    parity["max_rel_overlapped_exchange"] = float(np.max(np.abs(mine_chunked - ref) / ref))
+                    parity["max_rel"] = max(parity["max_rel"], parity["max_rel_overlapped_exchange"])
                 if world == 1 and K >= 2:
                     it_ms = res["iter_ms"][1:]
                     med = float(np.median(it_ms))
@@ -286,6 +329,7 @@ def main() -> int:
                 "exchange_ms_mean": round(st["exchange_ms_mean"], 4),
             },
             "exchange_ms_per_rank": [round(x, 4) for x in xchg_ms] if world > 1 else None,
+            "exchange_overlap_ab": overlap,
             "parity_max_rel": None if parity is None else parity["max_rel"],
             "parity": parity,
             "cpu_baseline": cpu,

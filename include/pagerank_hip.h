@@ -139,6 +139,14 @@ int pr_get_ranks(pr_graph *g, double *ranks_out);
 int pr_set_timing(pr_graph *g, int32_t enable);
 int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 
+/* Execution options (no effect on results; A/B and tuning).  PR_OPT_XCHG_CHUNKS: 1 = the
+ * exchange of a part with peers travels in one chunk per SpMV phase and the next iteration's
+ * phase c waits only for chunk c (overlap), 0 = whole runs (the default; PR_XCHG_CHUNKS sets it
+ * at build).  With RCCL every rank must make the same call (it is collective: the ranks check
+ * that they agree, so a mismatch fails instead of hanging); in a group, set every part alike. */
+#define PR_OPT_XCHG_CHUNKS 1
+int pr_set_option(pr_graph *g, int32_t option, int64_t value);
+
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes
  * to every rank (any channel), every rank attaches it to its part.  Once per iteration each
  * part sends every peer exactly the contributions (and the two dangling/L1 slots) that the

@@ -220,6 +220,16 @@ int pr_set_timing(pr_graph *g, int32_t enable) {
   return PR_OK;
 }
 
+int pr_set_option(pr_graph *g, int32_t option, int64_t value) {
+  if (!g) return fail(PR_ERR_INVALID, "NULL graph");
+  DeviceGuard dg(g->device);
+  if (option != PR_OPT_XCHG_CHUNKS) return fail(PR_ERR_INVALID, "unknown option");
+  PR_TRY(pr::join_exchange(g));  // a pending overlapped exchange finishes under the old setting
+  g->x_chunked = value != 0 && g->n_xc > 1;
+  if (g->comm && g->comm_size > 1) PR_TRY(pr::verify_exchange(g));  // collective: ranks must agree
+  return PR_OK;
+}
+
 int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
   if (!g || !stats) return fail(PR_ERR_INVALID, "NULL argument");
   DeviceGuard dg(g->device);
@@ -319,7 +329,6 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
   }
   g->comm_rank = rank;
   g->comm_size = n_ranks;
-  pr::set_exchange_chunking(g);
   if (n_ranks > 1) {
     const int rv = pr::verify_exchange(g);
     if (rv != PR_OK) {
@@ -363,7 +372,6 @@ int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, dou
     g->grouped = true;
     g->teleport = teleport;
     g->damping = damping;
-    pr::set_exchange_chunking(g);
     PR_TRY(pr::iter_reset(g, init_ranks));
   }
   PR_TRY(pr::group_exchange(parts, n_parts, 0));

@@ -250,8 +250,9 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
   PR_HIP(hipStreamSynchronize(s));
   // chunk bounds of the overlapped exchange: one chunk per hot phase (whether the chunks travel
-  // separately is decided when the transport is known: x_chunked, set_exchange_chunking)
+  // separately: x_chunked, PR_XCHG_CHUNKS / pr_set_option)
   g->n_xc = (g->C > 1 && g->hot_phased) ? std::max(1, g->C / kXcds) : 1;
+  set_exchange_chunking(g);
   PR_TRY(chunk_bounds(g, g->x_send.as<uint32_t>(), g->x_soff, true, &g->x_sch));
   PR_TRY(chunk_bounds(g, recv.as<uint32_t>(), g->x_roff, false, &g->x_rch));
   PR_HIP(hipStreamCreateWithFlags(&g->xstream, hipStreamNonBlocking));

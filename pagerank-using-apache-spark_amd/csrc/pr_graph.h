@@ -114,7 +114,7 @@ struct pr_graph {
   // the next iteration's phase c waits for x_ev[c] only (pr_iter.hip), so the transfer of the
   // later classes overlaps the SpMV of the earlier ones.
   int n_xc = 1;
-  // whether the chunks travel separately (PR_XCHG_CHUNKS=1, set at RCCL attach / group reset);
+  // whether the chunks travel separately (PR_XCHG_CHUNKS at build, pr_set_option later);
   // otherwise whole runs, and the next iteration waits for all of them
   bool x_chunked = false;
   std::vector<int64_t> x_sch, x_rch;

@@ -38,13 +38,14 @@ INFO_NAMES = ["n_vertices", "n_edges", "n_sink", "n_nolink", "n_indeg0", "max_in
 STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "iter_ms_mean",
               "build_ms", "exchange_ms_mean"]
 PR_CB_RANKS = 1
+PR_OPT_XCHG_CHUNKS = 1
 PR_COMM_ID_BYTES = 128
 
 # Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pr_abi_version", "pr_last_error", "pr_device_count", "pr_graph_create", "pr_graph_create_part",
     "pr_graph_info", "pr_graph_export_csr", "pr_run", "pr_reset", "pr_step", "pr_sync",
-    "pr_get_ranks", "pr_set_timing", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
+    "pr_get_ranks", "pr_set_timing", "pr_set_option", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
     "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_gen_chunglu", "pr_intern_device", "pr_group_reset",
     "pr_group_step", "pr_group_sync",
 ]
@@ -99,6 +100,7 @@ def load() -> ctypes.CDLL:
         "pr_sync": ([P], ctypes.c_int),
         "pr_get_ranks": ([P, P], ctypes.c_int),
         "pr_set_timing": ([P, i32], ctypes.c_int),
+        "pr_set_option": ([P, i32, i64], ctypes.c_int),
         "pr_get_stats": ([P, P, i32], ctypes.c_int),
         "pr_comm_unique_id": ([P], ctypes.c_int),
         "pr_graph_attach_comm": ([P, i32, i32, P], ctypes.c_int),

@@ -193,6 +193,11 @@ class PageRankGraph:
     def set_timing(self, enable: bool) -> None:
         check(_lib.load().pr_set_timing(self._h, 1 if enable else 0))
 
+    def set_exchange_chunks(self, on: bool) -> None:
+        """pr_set_option(PR_OPT_XCHG_CHUNKS): the exchange overlapped with the next iteration's
+        SpMV phases (True) or whole runs (False).  Collective with RCCL: every rank calls it."""
+        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_CHUNKS, 1 if on else 0))
+
     # -- multi-process -------------------------------------------------------------------------
     def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:
         buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES).from_buffer_copy(uid)

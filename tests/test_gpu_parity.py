@@ -483,12 +483,15 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
     csr = oracle_c.build_csr(V, src, dst)
     ref = oracle_c.run(csr, 9)
     out = {}
-    for chunks in ("on", "off"):
+    for chunks in ("on", "off", "opt"):
         monkeypatch.setenv("PR_XCHG_CHUNKS", "1" if chunks == "on" else "0")
         parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split")
                  for p in range(P)]
         try:
             assert all(p.info()["classes"] == 64 for p in parts)
+            if chunks == "opt":
+                for p in parts:
+                    p.set_exchange_chunks(True)
             grp = hip.PartGroup(parts)
             grp.reset()
             grp.step(4)
@@ -498,7 +501,7 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
         finally:
             for p in parts:
                 p.close()
-    assert np.array_equal(out["on"], out["off"])
+    assert np.array_equal(out["on"], out["off"]) and np.array_equal(out["opt"], out["off"])
     assert max_rel(out["on"], ref["ranks"]) <= RANK_TOL
 
 
