@@ -19,8 +19,9 @@ Rank 0 prints ONE JSON line (the driver's contract), including
                   rank's rows summed into one vector on rank 0 when N > 1) against K iterations
                   of the oracle on the exported canonical CSR -- the north-star 1e-9 bar;
   exchange_overlap_ab (N > 1): the K timed steps again with the exchange overlapped with the
-                  next iteration's SpMV phases (pr_set_option), beside the default's time; the
-                  parity leg then checks that mode too.
+                  next iteration's SpMV phases (pr_set_option), with 0/1/2 CUs per XCD kept free
+                  for the transfer kernels, beside the default's time; the parity leg then checks
+                  the overlapped mode too.
 """
 from __future__ import annotations
 
@@ -201,26 +202,34 @@ def main() -> int:
         xchg_ms = [float(x.item()) for x in allx]
 
     # N > 1: the same K steps again with the exchange overlapped (one chunk per SpMV phase,
-    # pr_set_option, collective), reported beside the default; the parity leg checks both modes
+    # pr_set_option, collective), with 0 / 1 / 2 CUs per XCD left free for the transfer kernels
+    # (they cannot share a CU with k_spmv_hot), reported beside the default; the parity leg
+    # checks the overlapped mode too
     overlap = None
     if dist is not None and info.get("classes", 1) >= 16 and not a.no_overlap_ab:
+        def timed_steps():
+            g.reset()
+            g.step(a.warmup)
+            g.sync()
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.step(a.steps)
+            g.sync()
+            torch.cuda.synchronize()
+            tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+            dist.barrier()
+            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+            return round(float(tc.item()) / max(a.steps, 1) * 1e3, 4)
+
+        overlap = {"unchunked_ms_per_step": round(ms_step, 4), "default": "unchunked",
+                   "chunks": info.get("classes", 1) // 8}
         g.set_exchange_chunks(True)
-        g.reset()
-        g.step(a.warmup)
-        g.sync()
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        g.step(a.steps)
-        g.sync()
-        torch.cuda.synchronize()
-        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-        dist.barrier()
-        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        for r in (0, 1, 2):
+            g.set_hot_reserve(r)
+            overlap[f"chunked_reserve{r}_ms_per_step"] = timed_steps()
+        g.set_hot_reserve(0)
         g.set_exchange_chunks(False)
-        overlap = {"unchunked_ms_per_step": round(ms_step, 4),
-                   "chunked_ms_per_step": round(float(tc.item()) / max(a.steps, 1) * 1e3, 4),
-                   "default": "unchunked", "chunks": info.get("classes", 1) // 8}
         log(f"exchange overlap A/B: {overlap}")
 
     # roofline of the dominant kernel group -- the SpMV pass (k_spmv_hot per column class,

@@ -145,6 +145,9 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
  * at build).  With RCCL every rank must make the same call (it is collective: the ranks check
  * that they agree, so a mismatch fails instead of hanging); in a group, set every part alike. */
 #define PR_OPT_XCHG_CHUNKS 1
+/* PR_OPT_HOT_RESERVE: CUs per XCD that the heavy SpMV kernel leaves free (0..3, default 0), for
+ * the overlapped exchange's transfer kernels, which cannot share a CU with it (LDS, registers). */
+#define PR_OPT_HOT_RESERVE 2
 int pr_set_option(pr_graph *g, int32_t option, int64_t value);
 
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes

@@ -223,6 +223,11 @@ int pr_set_timing(pr_graph *g, int32_t enable) {
 int pr_set_option(pr_graph *g, int32_t option, int64_t value) {
   if (!g) return fail(PR_ERR_INVALID, "NULL graph");
   DeviceGuard dg(g->device);
+  if (option == PR_OPT_HOT_RESERVE) {
+    if (value < 0 || value > 3) return fail(PR_ERR_INVALID, "PR_OPT_HOT_RESERVE: 0..3 CUs per XCD");
+    if (g->C > 1) PR_TRY(pr::set_hot_reserve(g, (int)value));
+    return PR_OK;
+  }
   if (option != PR_OPT_XCHG_CHUNKS) return fail(PR_ERR_INVALID, "unknown option");
   PR_TRY(pr::join_exchange(g));  // a pending overlapped exchange finishes under the old setting
   g->x_chunked = value != 0 && g->n_xc > 1;

@@ -668,7 +668,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     int wg_per_cu = 1;  // A/B knob: co-resident k_spmv_hot workgroups per CU (needs PR_HOT_SLOTS small enough)
     if (const char *e = getenv("PR_HOT_WGS_PER_CU")) wg_per_cu = std::min(std::max(atoi(e), 1), 4);
     g->hot_grid = std::max(C, n_cu * wg_per_cu / C * C);  // C | grid: every class gets the same CUs
+    g->hot_grid_full = g->hot_grid;
     g->hot_phased = hot_phased_setting();
+    if (const char *e = getenv("PR_HOT_RESERVE")) PR_TRY(set_hot_reserve(g, atoi(e)));  // A/B knob
 
     PR_TRY(prepare_hot_kernel());
     const int64_t nu = sp.n_units;

@@ -66,7 +66,8 @@ struct pr_graph {
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};
-  int hot_grid = 0;  // workgroups of k_spmv_hot (a multiple of C: one per CU)
+  int hot_grid = 0;       // workgroups of k_spmv_hot (a multiple of C: one per CU)
+  int hot_grid_full = 0;  // the same without reserved CUs (PR_OPT_HOT_RESERVE)
   bool hot_phased = false;  // an XCD's classes one after another (k_spmv_hot PHASED)
   bool hot_meta = false;    // lane metadata precomputed in hmeta (PR_HOT_META=1) instead of derived in-kernel
   bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
@@ -146,6 +147,9 @@ int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped ex
 // cannot share one -- and on one GPU the chunked group ran 8 % slower.
 void set_exchange_chunking(pr_graph *g);
 int n_hot_phases(const pr_graph *g);
+// k_spmv_hot leaves `per_xcd` CUs of every XCD free (phased schedule only: its grid need only be
+// a multiple of the XCD count)
+int set_hot_reserve(pr_graph *g, int per_xcd);
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
 int group_exchange(pr_graph *const *parts, int n, int buf);

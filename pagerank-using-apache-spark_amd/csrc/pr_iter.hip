@@ -166,6 +166,18 @@ int prepare_hot_kernel() {
 
 int n_hot_phases(const pr_graph *g) { return g->hot_phased ? std::max(1, g->C / kXcds) : 1; }
 
+int set_hot_reserve(pr_graph *g, int per_xcd) {
+  if (per_xcd == 0) {
+    g->hot_grid = g->hot_grid_full;
+    return PR_OK;
+  }
+  if (!g->hot_phased) return fail(PR_ERR_INVALID, "reserving CUs needs the phased k_spmv_hot schedule");
+  const int grid = g->hot_grid_full - kXcds * per_xcd;  // still a multiple of kXcds
+  if (per_xcd < 0 || grid < kXcds) return fail(PR_ERR_INVALID, "bad CU reserve");
+  g->hot_grid = grid;
+  return PR_OK;
+}
+
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   const size_t lds = g->hot.lds_bytes();
   auto *kern = g->hot_meta ? (g->hot_phased ? &k_spmv_hot<0, 0, 1, false> : &k_spmv_hot<0, 0, 0, false>)

@@ -39,6 +39,7 @@ STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "i
               "build_ms", "exchange_ms_mean"]
 PR_CB_RANKS = 1
 PR_OPT_XCHG_CHUNKS = 1
+PR_OPT_HOT_RESERVE = 2
 PR_COMM_ID_BYTES = 128
 
 # Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).

@@ -198,6 +198,10 @@ class PageRankGraph:
         SpMV phases (True) or whole runs (False).  Collective with RCCL: every rank calls it."""
         check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_CHUNKS, 1 if on else 0))
 
+    def set_hot_reserve(self, cus_per_xcd: int) -> None:
+        """pr_set_option(PR_OPT_HOT_RESERVE): CUs per XCD the heavy SpMV kernel leaves free."""
+        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_HOT_RESERVE, int(cus_per_xcd)))
+
     # -- multi-process -------------------------------------------------------------------------
     def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:
         buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES).from_buffer_copy(uid)

@@ -489,9 +489,10 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
                  for p in range(P)]
         try:
             assert all(p.info()["classes"] == 64 for p in parts)
-            if chunks == "opt":
+            if chunks == "opt":  # also with one CU per XCD left free (PR_OPT_HOT_RESERVE)
                 for p in parts:
                     p.set_exchange_chunks(True)
+                    p.set_hot_reserve(1)
             grp = hip.PartGroup(parts)
             grp.reset()
             grp.step(4)
