@@ -651,7 +651,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
-    if (const char *e = getenv("PR_HOT_ASSIGN")) hg.assign = std::min(2, std::max(0, atoi(e)));
+    if (const char *e = getenv("PR_HOT_ASSIGN")) hg.assign = std::min(3, std::max(0, atoi(e)));
     g->hot = hg;
     // hot-set gather positions per class, and the LDS slot of every hot gather position
     DevBuf hotidx;

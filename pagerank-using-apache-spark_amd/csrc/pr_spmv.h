@@ -427,6 +427,32 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   // staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced 512-byte
   // stores instead of eight scattered store instructions.
   const int e0 = (int)(meta >> kMetaExclShift), nseg = u.meta;
+  if constexpr (DIAG == 23) {
+    // every unit issues the same number of store instructions (all kWaveUnit / kStageSlots
+    // passes; the unused ones out of range), so the compiler can count them in the vmcnt waits
+    // for the next unit's gathers instead of waiting for these stores to complete
+#pragma unroll
+    for (int pass = 0; pass < kWaveUnit / kStageSlots; ++pass) {
+      const int base = pass * kStageSlots;
+      int e = e0 - base;
+      bool first = true;
+#pragma unroll
+      for (int j = 0; j < kWavePT; ++j) {
+        const bool end = (endm >> j) & 1u;
+        if (end && e >= 0 && e < kStageSlots) stage[e] = first ? __dadd_rn(carry, sv[j]) : sv[j];
+        if (end) first = false;
+        e += end ? 1 : 0;
+      }
+#pragma unroll
+      for (int h = 0; h < kStageSlots / kWave; ++h) {
+        const int i = h * kWave + lane_id();
+        const bool live = base + i < nseg;
+        const uint32_t o = live ? (uint32_t)(u.r0 + base + i) * 8u : 0xFFFFFFF8u;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i]), prs, o, 0, 2);
+      }
+    }
+    return;
+  }
   for (int base = 0; base < nseg; base += kStageSlots) {
     int e = e0 - base;
     bool first = true;
@@ -479,6 +505,19 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
     k = t0 + wv;
     stride = kWaves;
   }
+  // mode 3: the workgroup's units of mode 0 (every stride, kWaves consecutive ones) in the order
+  // its waves take them from the LDS counter hot[slots()] (zeroed before the class): a slow wave
+  // takes fewer units, so the waves reach the class's end together
+  const bool dyn = hg.assign == 3;
+  uint32_t *ctr = reinterpret_cast<uint32_t *>(const_cast<double *>(hot) + hg.slots());
+  const int lane = lane_id();
+  auto take = [&]() -> int64_t {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(ctr, 1u);
+    t = (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+    return beg + (int64_t)team * kWaves + (int64_t)(t % kWaves) + (int64_t)(t / kWaves) * stride;
+  };
+  if (dyn) k = take();
   if (k >= end) return;
   // unit descriptors through the scalar cache; index n_units (= ucum[kMaxClasses]) is an empty unit
   const __attribute__((address_space(4))) pr_v4i *cu = (const __attribute__((address_space(4))) pr_v4i *)units;
@@ -491,16 +530,17 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   Unit u[3];
   WaveCodes wc[3];
   double v[3][kWavePT];
+  int64_t k1 = dyn ? take() : k + stride;
   u[0] = unit_at(k);
   wave_unit_codes<MIK>(u[0], colh, hmeta, k, wc[0]);
-  u[1] = unit_at((k + stride < end) ? k + stride : none_k);
-  wave_unit_codes<MIK>(u[1], colh, hmeta, k + stride, wc[1]);
+  u[1] = unit_at(k1 < end ? k1 : none_k);
+  wave_unit_codes<MIK>(u[1], colh, hmeta, k1, wc[1]);
   wave_unit_gather<DIAG>(wc[0], hot, crs, v[0]);
   while (true) {
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl) {
       const int s1 = (sl + 1) % 3, s2 = (sl + 2) % 3;
-      const int64_t k2 = k + 2 * stride;
+      const int64_t k2 = dyn ? take() : k1 + stride;
       u[s2] = unit_at(k2 < end ? k2 : none_k);
       wave_unit_codes<MIK>(u[s2], colh, hmeta, k2, wc[s2]);
       if constexpr (ORDER == 0) {
@@ -510,7 +550,8 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
         wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
       }
-      k += stride;
+      k = k1;
+      k1 = k2;
       if (k >= end) return;
     }
   }
@@ -572,7 +613,10 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
         if (i < nh) hot[1 + i] = val[j];
       }
     }
-    if (threadIdx.x == 0) hot[0] = 0.0;
+    if (threadIdx.x == 0) {
+      hot[0] = 0.0;
+      *reinterpret_cast<uint32_t *>(hot + hg.slots()) = 0u;  // unit counter (PR_HOT_ASSIGN=3)
+    }
     __syncthreads();
     hot_class_units<ORDER, DIAG, MIK>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,
                                  piece_part, stage, wv);

@@ -523,3 +523,26 @@ def test_lane_metadata_in_kernel_equals_precomputed(hip, oracle_c, monkeypatch):
     assert np.array_equal(out["0"], out["1"])
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
     assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
+
+
+def test_unit_assignment_modes_bitwise(hip, oracle_c, monkeypatch):
+    """k_spmv_hot's unit -> wave mappings (PR_HOT_ASSIGN 0: interleaved over the XCD, 1: a run per
+    wave, 2: a run per workgroup, 3: the workgroup's waves take units from an LDS counter) and a
+    reserved CU per XCD (PR_HOT_RESERVE=1) only change which wave reduces a unit: bitwise equal
+    ranks, and the oracle's."""
+    monkeypatch.setenv("PR_CLASSES", "32")
+    monkeypatch.setenv("PR_HOT_SLOTS", "700")
+    rng = np.random.default_rng(77)
+    V = 50000
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.02)
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 7)
+    out = {}
+    for mode in ("0", "1", "2", "3", "3r"):
+        monkeypatch.setenv("PR_HOT_ASSIGN", mode[0])
+        monkeypatch.setenv("PR_HOT_RESERVE", "1" if mode.endswith("r") else "0")
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+            assert g.info()["classes"] == 32
+            out[mode], _ = g.run(7)
+    for mode in out:
+        assert np.array_equal(out[mode], out["0"]), mode
+    assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL

@@ -172,13 +172,15 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // partial stores, 4 / 5 = gathers folded into 4 / 32 MiB (1, 2, 4, 5: diagnostics, results wrong);
 // 13 / 14 / 15 = variants 0 / 1 / 4 with the reduce of unit i before the gathers of i+1;
 // 16..19 = phased schedule (the product's): product, all-LDS, all-LDS + an out-of-range buffer
-// load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, non-temporal
-// partial stores, every gather folded into the first 4 MiB.  The hot-set size is a build setting
+// load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, temporal
+// partial stores, every gather folded into the first 4 MiB; 23 = phased, the same number of
+// partial-store instructions for every unit (out-of-range ones for unused passes).
+// variant + 100 * a: with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[23] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[24] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -200,8 +202,12 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 14, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>)};
-  if (variant < 0 || variant > 22) return fail(PR_ERR_INVALID, "unknown variant");
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>)};
+  // variant + 100 * a: the same kernel with the unit assignment PR_HOT_ASSIGN = a (HotGeom.assign)
+  const int assign = variant / 100;
+  variant %= 100;
+  if (variant < 0 || variant > 23 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -209,6 +215,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   Unit *units = g->hunits.as<Unit>();
   int64_t *ucum = g->hucum.as<int64_t>();
   HotGeom hg = g->hot;
+  if (assign > 0) hg.assign = assign;
   uint32_t *colh = g->colh.as<uint32_t>(), *hmeta = g->hmeta.as<uint32_t>();
   double *cin = g->cbuf[0].as<double>(), *partial = g->partial.as<double>(), *pp = g->piece_part.as<double>();
   int64_t *poff = g->poff.as<int64_t>();

@@ -19,6 +19,9 @@ def main():
     ap.add_argument("--graph", default="rmat")
     ap.add_argument("--variants", default="0,1,2,3,4:19,4:22,4:24")
     ap.add_argument("--layout", default="fused", choices=["fused", "split"])
+    ap.add_argument("--parts", type=int, default=1,
+                    help="build the graph as this many row parts (a group on this GPU) and time part --part")
+    ap.add_argument("--part", type=int, default=0)
     a = ap.parse_args()
     import torch
 
@@ -32,19 +35,24 @@ def main():
     else:
         sparky_hip.gen_er(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=3)
     V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
-    g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E,
-                                 keep_canonical=False, layout=a.layout)
+    parts = [sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E,
+                                      keep_canonical=False, layout=a.layout, part=p, n_parts=a.parts)
+             for p in range(a.parts)]
     del s, d
     torch.cuda.empty_cache()
+    if a.parts > 1:
+        sparky_hip.PartGroup(parts).reset()
+    else:
+        parts[0].reset()
+    g = parts[a.part]
     info = g.info()
-    g.reset()
     D = ctypes.CDLL(os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpagerank_diag.so"))
     D.prd_time_spmv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double)]
     D.prd_time_split.argtypes = D.prd_time_spmv.argtypes
     fn = D.prd_time_split if a.layout == "split" else D.prd_time_spmv
     nbytes = 12 * info["local_edges"] + 36 * info["local_rows"]
-    print(f"graph {a.graph} s{a.scale}: V={V} E'={info['n_edges']} units={info['n_units']} "
+    print(f"graph {a.graph} s{a.scale} part {a.part}/{a.parts}: V={V} E'={info['n_edges']} units={info['n_units']} "
           f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
     variants = []
     for tok in a.variants.replace("+", ",").split(","):
@@ -67,7 +75,8 @@ def main():
         print(f"variant {t:>6}: median {med:8.3f} ms  min {x[0]:8.3f}  "
               f"{nbytes / (med * 1e-3) / 1e9:8.1f} GB/s model  {info['n_edges'] / (med * 1e-3) / 1e9:7.1f} GTEPS",
               flush=True)
-    g.close()
+    for p in parts:
+        p.close()
 
 
 if __name__ == "__main__":
