@@ -651,6 +651,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
+    // units reach waves through the workgroup's LDS counter: -3.5 % at s26, -0.7..-2.3 % per part
+    // at P = 2 / 8, -0.8 % at ER s24 against the static interleave (profiles/r02/assign_lds_ab/)
+    hg.assign = 3;
     if (const char *e = getenv("PR_HOT_ASSIGN")) hg.assign = std::min(3, std::max(0, atoi(e)));
     g->hot = hg;
     // hot-set gather positions per class, and the LDS slot of every hot gather position

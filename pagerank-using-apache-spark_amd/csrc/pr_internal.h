@@ -178,8 +178,8 @@ struct HotGeom {
   int64_t S_pad, Q_pad;
   // k_spmv_hot unit -> wave mapping (PR_HOT_ASSIGN A/B): 0 = the XCD's waves interleaved over
   // its class's units, 1 = one contiguous run of units per wave, 2 = one run per workgroup
-  // with its waves interleaved in it, 3 = the workgroup's units of mode 0 taken by its waves
-  // from an LDS counter (balanced within the workgroup)
+  // with its waves interleaved in it, 3 (the default) = the workgroup's units of mode 0 taken by
+  // its waves from an LDS counter (balanced within the workgroup)
   int assign;
   __host__ __device__ int slots() const { return P * Kp + 1; }
   // slot `slots()` is a control word (the workgroup's unit counter of PR_HOT_ASSIGN=3); the

@@ -175,7 +175,7 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, temporal
 // partial stores, every gather folded into the first 4 MiB; 23 = phased, the same number of
 // partial-store instructions for every unit (out-of-range ones for unused passes).
-// variant + 100 * a: with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
+// variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
@@ -204,8 +204,9 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>)};
-  // variant + 100 * a: the same kernel with the unit assignment PR_HOT_ASSIGN = a (HotGeom.assign)
-  const int assign = variant / 100;
+  // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
+  // (HotGeom.assign); a plain variant keeps the graph's own
+  const int assign = variant / 100 - 1;
   variant %= 100;
   if (variant < 0 || variant > 23 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
@@ -215,7 +216,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
   Unit *units = g->hunits.as<Unit>();
   int64_t *ucum = g->hucum.as<int64_t>();
   HotGeom hg = g->hot;
-  if (assign > 0) hg.assign = assign;
+  if (assign >= 0) hg.assign = assign;
   uint32_t *colh = g->colh.as<uint32_t>(), *hmeta = g->hmeta.as<uint32_t>();
   double *cin = g->cbuf[0].as<double>(), *partial = g->partial.as<double>(), *pp = g->piece_part.as<double>();
   int64_t *poff = g->poff.as<int64_t>();
