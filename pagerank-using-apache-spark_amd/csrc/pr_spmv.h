@@ -25,6 +25,10 @@
 
 namespace pr {
 
+// Diagnostics only (tools/diag, DIAG 24): per workgroup of k_spmv_hot the realtime clock at its
+// start and after every class phase ([b * 17 + 0] start, [b * 17 + 1 + ph] phase ph done).
+extern __device__ unsigned long long pr_diag_clock[];
+
 // dc = the parts' dangling partials added in part order (identical on every part)
 __device__ __forceinline__ double dc_from_slots(const double *cin, const SlotPos &sp) {
   double dc = 0.0;
@@ -491,6 +495,9 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   const int64_t beg = ucum[x];
   int64_t end = ucum[x + 1];
   constexpr int kWaves = kHotThreads / kWave;
+  // mode 3: the workgroup's slice of the class rotates with the phase, so a workgroup on a slower
+  // CU does not take the same slice of every class (-0.6 % at s26, -1.8 % per part at P = 8)
+  if (hg.assign == 3) team = (team + 5 * (x / kXcds)) % nteams;
   int64_t stride = (int64_t)nteams * kWaves;
   int64_t k = beg + (int64_t)team * kWaves + wv;
   if (hg.assign == 1) {  // a contiguous run of units per wave
@@ -580,6 +587,8 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   // PHASED: phases [ph0, ph1) of this launch (one launch per phase when the exchange overlaps)
   const int p_lo = PHASED ? ph0 : 0, p_hi = PHASED ? ph1 : 1;
+  if constexpr (DIAG == 24)
+    if (threadIdx.x == 0) pr_diag_clock[blockIdx.x * 17] = wall_clock64();
   for (int ph = p_lo; ph < p_hi; ++ph) {
     int x, team, nteams;
     if constexpr (PHASED) {
@@ -620,6 +629,10 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
     __syncthreads();
     hot_class_units<ORDER, DIAG, MIK>(x, team, nteams, units, ucum, hg, colh, hmeta, hot, crs, partial, poff,
                                  piece_part, stage, wv);
+    if constexpr (DIAG == 24) {  // phase done by every wave of this workgroup
+      __syncthreads();
+      if (threadIdx.x == 0) pr_diag_clock[blockIdx.x * 17 + 1 + ph] = wall_clock64();
+    }
   }
 }
 

@@ -11,6 +11,9 @@
 
 using namespace pr;
 
+// k_spmv_hot's DIAG 24 clock record (pr_spmv.h)
+__device__ unsigned long long pr::pr_diag_clock[4096 * 17];
+
 namespace {
 
 struct Layout {  // a work plan + padded columns for a given unit size
@@ -174,13 +177,21 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // 16..19 = phased schedule (the product's): product, all-LDS, all-LDS + an out-of-range buffer
 // load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, temporal
 // partial stores, every gather folded into the first 4 MiB; 23 = phased, the same number of
-// partial-store instructions for every unit (out-of-range ones for unused passes).
+// partial-store instructions for every unit (out-of-range ones for unused passes); 24 = the
+// product recording per-workgroup phase clocks (prd_clock_read).
 // variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
+// Copies n workgroups' clocks of the last DIAG 24 launch (17 per workgroup, 100 MHz ticks).
+int prd_clock_read(unsigned long long *out, int n) {
+  if (n < 0 || n > 4096) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pr_diag_clock), sizeof(unsigned long long) * 17 * (size_t)n, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[24] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[25] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -203,12 +214,13 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>)};
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 24, 1>)};
   // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
   // (HotGeom.assign); a plain variant keeps the graph's own
   const int assign = variant / 100 - 1;
   variant %= 100;
-  if (variant < 0 || variant > 23 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 24 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));

@@ -11,6 +11,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 
 
+def clock_summary(D, fn, g, variant=24):
+    """Workgroup clocks of one DIAG 24 launch (100 MHz): when every workgroup finished each class
+    phase, per XCD (workgroup b runs on XCD b % 8), and how long the CUs idle at the end."""
+    import numpy as np
+
+    ms = ctypes.c_double()
+    rc = fn(g._h, variant, 0xFFFFFFFF, 1, ctypes.byref(ms))
+    if rc != 0:
+        raise RuntimeError(f"clock variant: rc={rc}")
+    n = 4096
+    buf = (ctypes.c_ulonglong * (17 * n))()
+    D.prd_clock_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if D.prd_clock_read(buf, n) != 0:
+        raise RuntimeError("prd_clock_read failed")
+    c = np.frombuffer(buf, dtype=np.uint64).reshape(n, 17).astype(np.float64)
+    used = c[:, 0] > 0
+    c = c[used]
+    nwg = c.shape[0]
+    nph = int(np.max(np.sum(c[:, 1:] > 0, axis=1)))
+    t0 = c[:, 0].min()
+    ends = (c[:, 1:1 + nph] - t0) / 100.0  # us since the first workgroup started
+    span = ends[:, -1].max()
+    print(f"clock: {nwg} workgroups, {nph} phases, span {span:.1f} us (event {ms.value * 1e3:.1f} us)", flush=True)
+    xcd = np.arange(nwg) % 8
+    for ph in range(nph):
+        e = ends[:, ph]
+        per = [f"{e[xcd == k].min():7.1f}-{e[xcd == k].max():7.1f}" for k in range(8)]
+        print(f"  phase {ph}: done {e.min():7.1f}..{e.max():7.1f} us; per XCD " + " ".join(per), flush=True)
+    idle = float(np.mean(span - ends[:, -1]) / span)
+    print(f"  idle at the end: {idle * 100:.1f} % of the CU-time (last finisher {span:.1f} us, "
+          f"median {np.median(ends[:, -1]):.1f} us)", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=26)
@@ -22,6 +55,8 @@ def main():
     ap.add_argument("--parts", type=int, default=1,
                     help="build the graph as this many row parts (a group on this GPU) and time part --part")
     ap.add_argument("--part", type=int, default=0)
+    ap.add_argument("--clock", type=int, default=None, metavar="VARIANT",
+                    help="one launch of variant 24 (+ 100 * (assign + 1)): per-workgroup phase clocks summary")
     a = ap.parse_args()
     import torch
 
@@ -75,6 +110,8 @@ def main():
         print(f"variant {t:>6}: median {med:8.3f} ms  min {x[0]:8.3f}  "
               f"{nbytes / (med * 1e-3) / 1e9:8.1f} GB/s model  {info['n_edges'] / (med * 1e-3) / 1e9:7.1f} GTEPS",
               flush=True)
+    if a.clock is not None:
+        clock_summary(D, fn, g, a.clock)
     for p in parts:
         p.close()
 
