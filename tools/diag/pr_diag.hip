@@ -178,7 +178,9 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // load per entry, gathers without LDS reads; 20..22 = phased: no partial stores, temporal
 // partial stores, every gather folded into the first 4 MiB; 23 = phased, the same number of
 // partial-store instructions for every unit (out-of-range ones for unused passes); 24 = the
-// product recording per-workgroup phase clocks (prd_clock_read).
+// phased kernel (ORDER 0) recording per-workgroup phase clocks (prd_clock_read); 25 = phased
+// with the gathers of unit i + 1 issued before the reduce of unit i (ORDER 0, the product until
+// round 2; 16 is the product, ORDER 1; 17..24 keep ORDER 0).
 // variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 // Copies n workgroups' clocks of the last DIAG 24 launch (17 per workgroup, 100 MHz ticks).
@@ -191,7 +193,7 @@ int prd_clock_read(unsigned long long *out, int n) {
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[25] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[26] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -207,7 +209,7 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 4>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 13, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 14, 1>),
@@ -215,12 +217,13 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 24, 1>)};
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 24, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>)};
   // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
   // (HotGeom.assign); a plain variant keeps the graph's own
   const int assign = variant / 100 - 1;
   variant %= 100;
-  if (variant < 0 || variant > 24 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 25 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
