@@ -190,6 +190,40 @@ int prd_clock_read(unsigned long long *out, int n) {
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
 }
 
+// The grouped epilogue k_epilogue_grp<C, variant> alone, iters launches (rewrites r and the next
+// contribution buffer from the current one, like an iteration's epilogue; pr_reset afterwards).
+int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
+  if (g->C == 1 || !g->epi_grp) return fail(PR_ERR_STATE, "graph has no grouped epilogue");
+  if (variant < 0 || variant >= kNumEpiVariants) return fail(PR_ERR_INVALID, "unknown epilogue variant");
+  PR_HIP(hipSetDevice(g->device));
+  const EpiGrpFn epi = epi_grp_kernel(g->C, variant);
+  const size_t lds = epi_grp_lds(variant);
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const int G = kEpiVariants[variant].G;
+  const int blocks = (int)grid_for((g->nblk + G - 1) / G, kEpiThreads / kWave, 2048);
+  DevBuf part;
+  PR_TRY(part.alloc(sizeof(double2) * (size_t)blocks));
+  const int in = g->cur, out = g->cur ^ 1;
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  PR_HIP(hipEventRecord(a, g->stream));
+  for (int i = 0; i < iters; ++i)
+    hipLaunchKernelGGL(epi, dim3(blocks), dim3(kEpiThreads), lds, g->stream, g->nblk, g->partial.as<double>(),
+                       g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
+                       g->cbuf[out].as<double>() + g->own_off, g->cbuf[in].as<double>(), g->slots, (double)g->V,
+                       g->teleport, g->damping, part.as<double2>());
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipEventRecord(b, g->stream));
+  PR_HIP(hipEventSynchronize(b));
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  *ms_out = ms / iters;
+  return PR_OK;
+}
+
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");

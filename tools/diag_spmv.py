@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--parts", type=int, default=1,
                     help="build the graph as this many row parts (a group on this GPU) and time part --part")
     ap.add_argument("--part", type=int, default=0)
+    ap.add_argument("--epi", action="store_true",
+                    help="time k_epilogue_grp variants (pr_internal.h kEpiVariants) instead of k_spmv_hot")
     ap.add_argument("--clock", type=int, default=None, metavar="VARIANT",
                     help="one launch of variant 24 (+ 100 * (assign + 1)): per-workgroup phase clocks summary")
     a = ap.parse_args()
@@ -86,6 +88,9 @@ def main():
                                 ctypes.POINTER(ctypes.c_double)]
     D.prd_time_split.argtypes = D.prd_time_spmv.argtypes
     fn = D.prd_time_split if a.layout == "split" else D.prd_time_spmv
+    if a.epi:
+        D.prd_time_epi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        fn = lambda h, v, m, it, out: D.prd_time_epi(h, v, it, out)  # noqa: E731
     nbytes = 12 * info["local_edges"] + 36 * info["local_rows"]
     print(f"graph {a.graph} s{a.scale} part {a.part}/{a.parts}: V={V} E'={info['n_edges']} units={info['n_units']} "
           f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
