@@ -110,8 +110,10 @@ constexpr int kEpiThreads = 256;      // 4 waves, 32.1 KiB of LDS: four workgrou
 // (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
 struct EpiVariant {
   int G, W;
+  bool legacy = false;  // round-1 staging loop (per-class fill accounting) instead of the prefix batches
 };
-constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016}};
+constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016},
+                                       {kEpiGroup, kEpiWin, true}};
 constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);
 
 // per-row info word: out-degree | flags

@@ -321,6 +321,20 @@ __device__ __forceinline__ int dpp_i32(int x) {
   return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
 }
 
+// Inclusive wave64 scan of an int (row_shr 1/2/4/8, then row_bcast 15/31).
+__device__ __forceinline__ int wave_incl_scan_i32(int x) {
+  const int row = lane_id() >> 4;
+  x += dpp_i32<0x111>(x);
+  x += dpp_i32<0x112>(x);
+  x += dpp_i32<0x114>(x);
+  x += dpp_i32<0x118>(x);
+  int p = dpp_i32<0x142>(x);
+  if (row == 1 || row == 3) x += p;
+  p = dpp_i32<0x143>(x);
+  if (row >= 2) x += p;
+  return x;
+}
+
 // The lane metadata of a STREAM unit (pr_internal.h) from the end marks in bit 0 of its codes:
 // which of the lane's entries end a segment, the six "add the partner" predicates of the wave's
 // segmented scan (the partner lanes up to this one hold no segment end), and the index of the
@@ -749,7 +763,7 @@ __device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t b
 // row's position in the staged run and the row adds it from LDS (epi_class_add).  Runs start at
 // even slots (16-byte alignment): slot s of a run staged at window offset f sits at
 // f + s - (s & ~1).  Each wave's window is W slots plus a zero slot (and one of padding).
-template <int C, int G = kEpiGroup, int W = kEpiWin>
+template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false>
 __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
@@ -802,6 +816,40 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
     auto run_end = [&](int y) {
       return (C <= kWave || y < kWave) ? __builtin_amdgcn_readlane(ce, y) : __builtin_amdgcn_readlane(ce1, y - kWave);
     };
+    if constexpr (C <= kWave && !LEGACY) {
+      // lane y: class y's run start rounded down to 16 bytes (sa), its staged length n2 (0: no
+      // slots in this group) and its window position, the exclusive prefix of n2 over the
+      // classes.  A batch is the longest sequence of classes from x0 whose staged runs fit the
+      // window (one ballot), so the per-class work is a readlane or two and the DMA itself.
+      const int sa = cs & ~1;
+      const int n2 = (lane < C && ce > cs) ? (((ce + 1) & ~1) - sa) : 0;
+      const int incl = wave_incl_scan_i32(n2);
+      const int pre = incl - n2;
+      const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
+      for (int x0 = 0; x0 < C;) {
+        const int base = __builtin_amdgcn_readlane(pre, x0);
+        const unsigned long long over = __ballot(lane >= x0 && lane < C && incl - base > W);
+        const int x1 = over ? (int)__builtin_ctzll(over) : C;  // > x0: one run always fits
+        for (int y = x0; y < x1; ++y) {
+          const int n = __builtin_amdgcn_readlane(n2, y);
+          if (n == 0) continue;
+          const double *src = partial + __builtin_amdgcn_readlane(sa, y);
+          double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
+          for (int o = 0; o < n; o += 2 * kWave)
+            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
+        for (int y = x0; y < x1; ++y) {
+          if (__builtin_amdgcn_readlane(n2, y) == 0) continue;
+          const uint32_t bit = 1u << (y & 31);
+          const int run = __builtin_amdgcn_readlane(roff, y) - base;
+          if (MW == 1 || y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
+          else epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+        x0 = x1;
+      }
+    } else {
     for (int x = 0; x < C;) {
       // stage the runs of classes [x, xe) that fit the window (at least one always does)
       int fill = 0, xe = x;
@@ -832,6 +880,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       }
       __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
       x = xe;
+    }
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -867,6 +916,7 @@ inline EpiGrpFn epi_grp_kernel_c(int var) {
     case 3: return k_epilogue_grp<C, kEpiVariants[3].G, kEpiVariants[3].W>;
     case 4: return k_epilogue_grp<C, kEpiVariants[4].G, kEpiVariants[4].W>;
     case 5: return k_epilogue_grp<C, kEpiVariants[5].G, kEpiVariants[5].W>;
+    case 6: return k_epilogue_grp<C, kEpiVariants[6].G, kEpiVariants[6].W, kEpiVariants[6].legacy>;
     default: return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W>;
   }
 }

@@ -293,7 +293,8 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
                                                              (32, "1", "1", "v4"), (64, "0", "1", "1"),
                                                              (64, "1", "1", "1"), (64, "1", "1", "v2"),
                                                              (64, "1", "0", "1"), (128, "0", "1", "1"),
-                                                             (128, "1", "1", "1"), (128, "1", "0", "v2")])
+                                                             (128, "1", "1", "1"), (128, "1", "0", "v2"),
+                                                             (64, "1", "1", "v6")])
 def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp, monkeypatch):
     """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
     after another with the hot set restaged per class) and the three epilogues: grouped (class
@@ -545,4 +546,24 @@ def test_unit_assignment_modes_bitwise(hip, oracle_c, monkeypatch):
             out[mode], _ = g.run(7)
     for mode in out:
         assert np.array_equal(out[mode], out["0"]), mode
+    assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
+
+
+def test_epilogue_staging_modes_bitwise(hip, oracle_c, monkeypatch):
+    """k_epilogue_grp stages a group's class runs by prefix batches (one ballot per window load)
+    or, PR_EPI_VAR=6, by the round-1 per-class fill loop: the same runs at the same window
+    positions, so the row sums -- and the ranks -- are bitwise equal."""
+    monkeypatch.setenv("PR_CLASSES", "64")
+    monkeypatch.setenv("PR_HOT_SLOTS", "400")
+    rng = np.random.default_rng(31)
+    V = 70000
+    src, dst = random_edges(rng, V, 900000, hub_frac=0.03)
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 6)
+    out = {}
+    for var in ("0", "6"):
+        monkeypatch.setenv("PR_EPI_VAR", var)
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+            assert g.info()["classes"] == 64 and g.info()["epilogue"] == 3
+            out[var], _ = g.run(6)
+    assert np.array_equal(out["0"], out["6"])
     assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL

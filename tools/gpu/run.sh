@@ -5,7 +5,7 @@
 # Steps run in order, each under its own time limit, and the script stops at the first failure
 # (no GPU step runs after a fault, abort or timeout).  Output goes to gpurun_out/<tag>/.
 #   pytest            python -m pytest tests -m gpu (everything, -x, per-test timeout)
-#   pytest:<expr>     the same restricted with -k <expr>
+#   pytest:<expr>     the same restricted with -k <expr> ('+' between names: ' or ')
 #   smoke             __graft_entry__.smoke()
 #   bench[:args]      python bench.py <args, ',' for ' '>        (log: bench_<n>.log)
 #   trace[:args]      rocprofv3 --kernel-trace --stats on bench.py --no-cpu-baseline <args>
@@ -33,7 +33,7 @@ for step in "$@"; do
   echo "[run.sh] step $n: ${envs[*]} $name $args" | tee -a $O/steps.txt
   case $name in
     pytest)
-      if [ -n "$arg" ]; then k=(-k "$arg"); else k=(); fi
+      if [ -n "$arg" ]; then k=(-k "${arg//+/ or }"); else k=(); fi
       env "${envs[@]}" timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 || exit 1 ;;
     smoke)
       env "${envs[@]}" timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 || exit 1 ;;
