@@ -71,7 +71,8 @@ extern "C" {
 #define PR_INFO_PARTIAL_SLOTS 16 /* (row, column class) segment sums of the split layout     */
 #define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
 #define PR_INFO_EPILOGUE 18    /* 0 fused, 1 per-block, 2 per-class buffers, 3 grouped      */
-#define PR_INFO_COUNT 19
+#define PR_INFO_GATHER_EST 19  /* bytes of the part's expected gather space (class policy)   */
+#define PR_INFO_COUNT 20
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

@@ -156,7 +156,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2))};
+                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2)), g->gather_est};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

@@ -114,6 +114,20 @@ __global__ void k_vflags(int32_t V, const uint8_t *__restrict__ is_key,
   atomicMax(&cnt[4], mo);
 }
 
+// Expected number of peers' sources a part reads (class policy at P > 1): a source with d
+// out-links is read by a given other part with probability 1 - (1 - 1/P)^d (its out-links land
+// in random parts: parts own every P-th vertex of the degree order).  Summed in fixed point
+// (2^-20) with integer atomics, so every part computes the same value.
+__global__ void k_reader_est(int32_t V, int P, const int32_t *__restrict__ deg, unsigned long long *__restrict__ sum) {
+  const double q = 1.0 - 1.0 / (double)P;
+  unsigned long long acc = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < V; v += (int64_t)gridDim.x * blockDim.x) {
+    const int d = deg[v];
+    if (d > 0) acc += (unsigned long long)((1.0 - pow(q, (double)d)) * 1048576.0);
+  }
+  atomicAdd(sum, acc);
+}
+
 // Internal order key: out-degree descending, original ID ascending (hot contributions first).
 __global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
                              uint64_t *__restrict__ vk) {
@@ -382,18 +396,22 @@ __global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *_
   }
 }
 
-// Tuning knobs read at build time (DESIGN.md §8).
-// Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the gather
-// space fits 3/4 of one XCD's 4 MiB L2 (the phased schedule runs one class per XCD at a time; the
-// rest of the L2 carries the streamed codes and metadata), capped at kAutoMaxClasses; PR_CLASSES
-// overrides.  R-MAT s26 (262 MB) -> 64, ER s24 (134 MB) -> 64, LiveJournal (39 MB) -> 16.
+// Tuning knobs read at build time (DESIGN.md §9).
+// Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the part's
+// gather space (its slice plus the expected received runs at P > 1) fits one XCD's 4 MiB L2 (the
+// phased schedule runs one class per XCD at a time), capped at kAutoMaxClasses; PR_CLASSES
+// overrides.  More classes keep more gathers in L2 and the LDS hot sets but cost epilogue work per
+// (row, class): R-MAT s26 (262 MB) -> 64 at P = 1, 2, 4 and 32 for an 8-way part (121 MB: 8 % less
+// per iteration than 64); the Twitter shape stays at 64 at P = 8 (6 % better than 32); ER s24
+// (134 MB) -> 64, LiveJournal (39 MB) -> 16 (profiles/r02/class_policy/).
+constexpr int64_t kClassRegionBytes = 4000000;  // just under the 4 MiB L2: ER s24 (4.19 MB at 32) stays at 64
 static int class_setting(int64_t gather_bytes) {
   if (const char *e = getenv("PR_CLASSES")) {
     const int c = atoi(e);
     return (c == 8 || c == 16 || c == 64 || c == 128) ? c : 32;
   }
   for (int c = kXcds; c < kAutoMaxClasses; c *= 2)
-    if (gather_bytes * 4 <= (int64_t)c * kL2BytesPerXcd * 3) return c;
+    if (gather_bytes <= (int64_t)c * kClassRegionBytes) return c;
   return kAutoMaxClasses;
 }
 
@@ -501,8 +519,20 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   g->n_local = V > part ? (V - part + P - 1) / P : 0;
   if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
   // Column classes when the gather space (every part's slice: the columns a part reads) outgrows
-  // the L2s (pr_graph.h).
-  const int c_split = class_setting((int64_t)P * g->n_local_max * 8);
+  // the L2s (pr_graph.h); their count from the part's expected compacted gather space.
+  int64_t gather_est = g->n_local_max * 8;
+  if (P > 1 && V > 0) {
+    PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_reader_est, dim3(grid_for(V, T, 1024)), dim3(T), 0, s, V, P, c_deg.as<int32_t>(),
+                       cnt.as<unsigned long long>());
+    PR_HIP(hipGetLastError());
+    unsigned long long est = 0;
+    PR_HIP(hipMemcpyAsync(&est, cnt.p, sizeof(est), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
+    gather_est += (int64_t)((double)est / 1048576.0 * (double)(P - 1) / (double)P) * 8;
+  }
+  g->gather_est = gather_est;
+  const int c_split = class_setting(gather_est);
   int C = ((int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
   if (g->flags & PR_LAYOUT_FUSED) C = 1;
   if (g->flags & PR_LAYOUT_SPLIT) C = c_split;

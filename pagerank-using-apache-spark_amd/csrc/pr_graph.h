@@ -42,6 +42,7 @@ struct pr_graph {
   int64_t n_local = 0;      // rows owned (without holes)
   int64_t n_rows = 0;       // C * Q_pad local rows (with holes)
   int C = 1;                // column classes
+  int64_t gather_est = 0;   // expected gather-space bytes the class count was chosen from
   int64_t Q_pad = 0;        // rows per class region
   int64_t n_local_max = 0;  // ceil(V / P)
   int64_t S_pad = 0;        // doubles per gather slice

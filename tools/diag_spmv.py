@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--graph", default="rmat")
+    ap.add_argument("--graph", default="rmat", choices=["rmat", "er", "lj", "twitter"])
     ap.add_argument("--variants", default="0,1,2,3,4:19,4:22,4:24")
     ap.add_argument("--layout", default="fused", choices=["fused", "split"])
     ap.add_argument("--parts", type=int, default=1,
@@ -64,18 +64,14 @@ def main():
 
     import sparky_hip
 
-    E = 16 << a.scale
-    s = torch.empty(E, dtype=torch.int32, device="cuda")
-    d = torch.empty(E, dtype=torch.int32, device="cuda")
-    if a.graph == "rmat":
-        sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=2)
-    else:
-        sparky_hip.gen_er(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=3)
-    V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    from sparky_hip.workloads import generate
+
+    wl = generate(a.graph, scale=a.scale, device=0)  # the bench's workloads (rmat seed 2 at s26, er 3, ...)
+    s, d, E, V = wl.src, wl.dst, wl.n_edges, wl.n_vertices
     parts = [sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E,
                                       keep_canonical=False, layout=a.layout, part=p, n_parts=a.parts)
              for p in range(a.parts)]
-    del s, d
+    del s, d, wl
     torch.cuda.empty_cache()
     if a.parts > 1:
         sparky_hip.PartGroup(parts).reset()
@@ -93,7 +89,7 @@ def main():
         fn = lambda h, v, m, it, out: D.prd_time_epi(h, v, it, out)  # noqa: E731
     nbytes = 12 * info["local_edges"] + 36 * info["local_rows"]
     print(f"graph {a.graph} s{a.scale} part {a.part}/{a.parts}: V={V} E'={info['n_edges']} units={info['n_units']} "
-          f"long_rows={info['n_long_rows']} model_bytes={nbytes / 1e9:.2f} GB", flush=True)
+          f"long_rows={info['n_long_rows']} classes={info['classes']} gather_est={info['gather_est'] / 1e6:.1f}MB model_bytes={nbytes / 1e9:.2f} GB", flush=True)
     variants = []
     for tok in a.variants.replace("+", ",").split(","):
         if ":" in tok:
