@@ -14,7 +14,7 @@
 //   r       fp64[R]           ranks, updated in place
 //
 // Column classes (C = 8..64 once the whole gather space passes 4 MiB -- the fewest whose class
-// region fits 3/4 of one XCD's L2 -- else C = 1): local rank j -> class x = j % C, row
+// region of the part's expected gather space is <= 4 MB -- else C = 1): local rank j -> class x = j % C, row
 // L = x*Q_pad + j/C (also its position in the slice).  Split layout (C > 1): every row's in-links
 // are split by the class of their source; each non-empty (row, class) pair is a segment with one
 // slot of a class-dense partial array.  Class-x wave units run on XCD x % 8, one class after
