@@ -79,7 +79,8 @@ def main():
         parts[0].reset()
     g = parts[a.part]
     info = g.info()
-    D = ctypes.CDLL(os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpagerank_diag.so"))
+    D = ctypes.CDLL(os.environ.get("PR_DIAG_LIB") or
+                    os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpagerank_diag.so"))
     D.prd_time_spmv.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_double)]
     D.prd_time_split.argtypes = D.prd_time_spmv.argtypes
