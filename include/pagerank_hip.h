@@ -72,7 +72,8 @@ extern "C" {
 #define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
 #define PR_INFO_EPILOGUE 18    /* 0 fused, 1 per-block, 2 per-class buffers, 3 grouped      */
 #define PR_INFO_GATHER_EST 19  /* bytes of the part's expected gather space (class policy)   */
-#define PR_INFO_COUNT 20
+#define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
+#define PR_INFO_COUNT 21
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

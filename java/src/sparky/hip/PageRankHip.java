@@ -29,7 +29,7 @@ public final class PageRankHip implements AutoCloseable {
     /** pr_graph_create flags (include/pagerank_hip.h). */
     public static final int PR_DANGLING_LOCAL = 0, PR_DANGLING_NONE = 1, PR_NO_CANONICAL = 4;
     static final int PR_CB_RANKS = 1;
-    static final int PR_INFO_COUNT = 20;
+    static final int PR_INFO_COUNT = 21;
 
     /** Per-iteration hook: ranks is null unless requested (original-ID order, V doubles). */
     @FunctionalInterface

@@ -43,7 +43,7 @@ void DevBuf::reset() {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + ewalk.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
   return b;
@@ -156,7 +156,8 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2)), g->gather_est};
+                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2)), g->gather_est,
+                                    g->n_walk_groups};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

@@ -670,6 +670,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(sp.units_plan(s));
     g->rmask = std::move(sp.rmask);
     g->cbase = std::move(sp.cbase);
+    PR_TRY(plan_epi_walk(g));
     pieces = sp.n_pieces;
     if (sp.entries / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
     // LDS hot set per class, then the entry codes

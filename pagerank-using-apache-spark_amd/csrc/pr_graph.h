@@ -74,6 +74,11 @@ struct pr_graph {
   bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
   bool epi_grp = false;     // epi_abs + a sentinel cbase row: k_epilogue_grp (LDS-staged class runs)
   int epi_var = 0;          // its (group, window) variant, pr_spmv.h kEpiVariants (PR_EPI_VAR)
+  // per-row walk of sparse groups in k_epilogue_grp (PR_EPI_WALK): per group a flag (ewalk, u8)
+  // and, for walking groups, every slot's window position in row-major order (epos, u16 [group][W])
+  bool epi_walk = false;
+  int64_t n_walk_groups = 0;
+  pr::DevBuf ewalk, epos;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
   pr::DevBuf cbuf[2];
@@ -138,6 +143,7 @@ struct pr_graph {
 namespace pr {
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
+int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (after rmask/cbase)
 int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);

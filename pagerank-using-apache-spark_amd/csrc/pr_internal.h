@@ -113,7 +113,7 @@ struct EpiVariant {
   bool legacy = false;  // round-1 staging loop (per-class fill accounting) instead of the prefix batches
 };
 constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016},
-                                       {kEpiGroup, kEpiWin, true}};
+                                       {kEpiGroup, kEpiWin, true}, {8, 1272}};
 constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);
 
 // per-row info word: out-degree | flags

@@ -154,13 +154,51 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 int prepare_hot_kernel() {
   for (int v = 0; v < kNumEpiVariants; ++v)
     for (int c : {8, 16, 32, 64, 128})
-      PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v)),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
+      for (bool walk : {false, true})
+        PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v, walk)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
   for (const void *k : {reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, true>),
                         reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1, true>),
                         reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, false>),
                         reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1, false>)})
     PR_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  return PR_OK;
+}
+
+// The per-row walk of sparse epilogue groups (pr_spmv.h k_epilogue_grp WALK): on by default for
+// the grouped epilogue's variants 0 and 7 at <= 64 classes; PR_EPI_WALK=0 keeps the class loop
+// everywhere (A/B).  Plans which groups walk and their slots' window positions.
+int plan_epi_walk(pr_graph *g) {
+  g->epi_walk = false;
+  g->n_walk_groups = 0;
+  bool on = true;
+  if (const char *e = getenv("PR_EPI_WALK")) on = atoi(e) != 0;
+  if (!on || !g->epi_grp || !epi_walk_variant(g->C, g->epi_var) || g->nblk <= 0) return PR_OK;
+  const int G = kEpiVariants[g->epi_var].G, W = kEpiVariants[g->epi_var].W;
+  const int64_t ngrp = (g->nblk + G - 1) / G;
+  PR_TRY(g->ewalk.alloc((size_t)ngrp));
+  PR_TRY(g->epos.alloc(sizeof(uint16_t) * (size_t)ngrp * W));
+  const unsigned blocks = grid_for(ngrp, kEpiThreads / kWave, 8192);
+  using PlanFn = void (*)(int64_t, const void *, const int32_t *, uint8_t *, uint16_t *);
+  PlanFn fn = nullptr;
+  const bool wide = g->epi_var == 7;
+  switch (g->C) {
+    case 8: fn = wide ? k_epi_walk_plan<8, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<8, kEpiGroup, kEpiWin>; break;
+    case 16: fn = wide ? k_epi_walk_plan<16, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<16, kEpiGroup, kEpiWin>; break;
+    case 32: fn = wide ? k_epi_walk_plan<32, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<32, kEpiGroup, kEpiWin>; break;
+    case 64: fn = wide ? k_epi_walk_plan<64, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<64, kEpiGroup, kEpiWin>; break;
+    default: return PR_OK;
+  }
+  static_assert(kEpiVariants[0].G == kEpiGroup && kEpiVariants[0].W == kEpiWin, "variant 0 is the default");
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p, g->cbase.as<int32_t>(),
+                     g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
+  PR_HIP(hipGetLastError());
+  std::vector<uint8_t> flags((size_t)ngrp);
+  PR_HIP(hipMemcpyAsync(flags.data(), g->ewalk.p, (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  g->n_walk_groups = 0;
+  for (uint8_t f : flags) g->n_walk_groups += f;
+  g->epi_walk = true;
   return PR_OK;
 }
 
@@ -278,12 +316,13 @@ int iter_compute(pr_graph *g) {
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
     if (g->epi_grp) {
-      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var);
+      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var, g->epi_walk);
       const size_t lds = epi_grp_lds(g->epi_var);
       hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(kEpiThreads), lds, s, g->nblk, g->partial.as<double>(),
                          g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                          g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
-                         (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units);
+                         (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
+                         g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
     } else {
     auto *epi = g->epi_abs ? (g->C == 32 ? k_epilogue<32, true> : (g->C == 16 ? k_epilogue<16, true> : k_epilogue<8, true>))
                            : (g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>));

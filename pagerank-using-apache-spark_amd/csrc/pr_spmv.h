@@ -374,7 +374,10 @@ __device__ __forceinline__ uint32_t derive_meta(const WaveCodes &w) {
 // gather-space loads), 2 = no partial stores, 3 = temporal (default-policy) partial stores, 4 / 5 = every
 // gather-space load folded into the first 4 / 32 MiB (L2- / Infinity-Cache-resident), 6 =
 // exec-masked gathers, 8 = every gather instruction reads 512 contiguous bytes, 13 = every value
-// from LDS plus an out-of-range buffer load per entry, 14 = no LDS reads (gathers only).
+// from LDS plus an out-of-range buffer load per entry, 14 = no LDS reads (gathers only), 30 = every
+// partial store folded into one 256 KiB window (wave_unit_reduce), 31 = the product (was: 16-byte
+// partial stores before they became the product's), 32 / 33 = carry through the staging window,
+// 34 = one 8-byte partial store per slot (the product until round 3).
 template <int DIAG>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, __amdgpu_buffer_rsrc_t crs,
                                                  double (&v)[kWavePT]) {
@@ -404,10 +407,23 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
   }
 }
 
-template <int DIAG, bool MIK>
+// The stores of one staged pass: slots [base, base + n) of the unit from the wave's window.
+template <int DIAG>
+__device__ __forceinline__ void store_staged(const Unit &u, __amdgpu_buffer_rsrc_t prs, const double *stage, int base,
+                                             int n) {
+  for (int i = lane_id(); i < n; i += kWave) {
+    const uint32_t o = (uint32_t)(u.r0 + base + i) * 8u;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i]), prs, o, 0, 2);
+  }
+}
+
+// DEFER (diagnostics, ORDER 3): the last staged pass is not stored here; *dbase / *dn say which
+// slots the caller stores later (store_staged) -- after the next unit's gathers are issued.
+template <int DIAG, bool MIK, bool DEFER = false>
 __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
                                                  __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
-                                                 double *stage) {
+                                                 double *stage, int *dbase = nullptr, int *dn = nullptr) {
+  if constexpr (DEFER) *dn = 0;
   if (u.meta < 0) {  // PIECE of a long segment
     double acc = 0.0;
 #pragma unroll
@@ -471,8 +487,25 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     }
     return;
   }
-  for (int base = 0; base < nseg; base += kStageSlots) {
+  // DIAG 32: the carry is added to the lane's first end through the window (one add instead of
+  // one per entry); DIAG 33: the same with unconditional window writes (non-ends to a spare slot)
+  constexpr int kCap = DIAG == 33 ? kStageSlots - 1 : kStageSlots;
+  for (int base = 0; base < nseg; base += kCap) {
     int e = e0 - base;
+    if constexpr (DIAG == 32 || DIAG == 33) {
+#pragma unroll
+      for (int j = 0; j < kWavePT; ++j) {
+        const bool end = (endm >> j) & 1u;
+        if constexpr (DIAG == 33) {
+          stage[(end && e >= 0 && e < kCap) ? e : kCap] = sv[j];
+        } else {
+          if (end && e >= 0 && e < kCap) stage[e] = sv[j];
+        }
+        e += end ? 1 : 0;
+      }
+      const int f = e0 - base;
+      if (endm != 0u && f >= 0 && f < kCap) stage[f] = __dadd_rn(carry, stage[f]);
+    } else {
     bool first = true;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) {
@@ -481,9 +514,33 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
       if (end) first = false;
       e += end ? 1 : 0;
     }
-    const int n = min(kStageSlots, nseg - base);
+    }
+    const int n = min(kCap, nseg - base);
+    if constexpr (DEFER) {
+      if (base + kCap >= nseg) {  // the last pass: stored by the caller
+        *dbase = base;
+        *dn = n;
+        continue;
+      }
+    }
+    // two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an odd
+    // last slot alone: half the store instructions of one 8-byte store per slot (-1.7 % at s26,
+    // profiles/r03/; DIAG 34 keeps the 8-byte stores for A/B)
+    if constexpr (!(DIAG == 2 || DIAG == 3 || DIAG == 30 || DIAG == 34)) {
+      static_assert(kStageSlots <= 2 * kWave, "one b128 pass");
+      const int i2 = 2 * lane_id();
+      const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
+      if (i2 + 1 < n) {
+        const pr_v4i q = *reinterpret_cast<const pr_v4i *>(stage + i2);
+        __builtin_amdgcn_raw_buffer_store_b128(q, prs, o, 0, 2);
+      } else if (i2 < n) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i2]), prs, o, 0, 2);
+      }
+      continue;
+    }
     for (int i = lane_id(); i < n; i += kWave) {
-      const uint32_t o = (uint32_t)(u.r0 + base + i) * 8u;
+      uint32_t o = (uint32_t)(u.r0 + base + i) * 8u;
+      if constexpr (DIAG == 30) o &= 0x3FFF8u;  // every partial store into one 256 KiB (L2-resident) window
       // non-temporal (nt): the partials are read back by the epilogue only after every class
       // has run, so they should not evict the class region from L2 (5 % of the kernel at s26;
       // DIAG 3 = the temporal stores of round 1, profiles/r02/experiments.md)
@@ -567,6 +624,11 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       if constexpr (ORDER == 0) {
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
         wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+      } else if constexpr (ORDER == 3) {  // diagnostics: the last staged stores after the next gathers
+        int db = 0, dn = 0;
+        wave_unit_reduce<DIAG, MIK, true>(u[sl], wc[sl], v[sl], prs, piece_part, stage, &db, &dn);
+        wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
+        store_staged<DIAG>(u[sl], prs, stage, db, dn);
       } else {  // reduce first: a gather issue stalled by a busy address unit cannot hold it up
         wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
@@ -763,12 +825,21 @@ __device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t b
 // row's position in the staged run and the row adds it from LDS (epi_class_add).  Runs start at
 // even slots (16-byte alignment): slot s of a run staged at window offset f sits at
 // f + s - (s & ~1).  Each wave's window is W slots plus a zero slot (and one of padding).
-template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false>
-__global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
+//
+// WALK (per-row walk of sparse groups, PR_EPI_WALK): a group the build marked in ewalk has all of
+// its class runs in one window load, followed in the window by the u16 window positions of its
+// slots in row-major order (epos, planned by k_epi_walk_plan with the same staging rules).  Each
+// row then adds only its own slots, in class order -- as many steps as the block's busiest row
+// has classes instead of C (R-MAT s26: most rows have one or two) -- and the sums are bitwise
+// those of the class loop (the loop's absent classes add an exact +0).
+// (4 waves per SIMD: the LDS of four workgroups per CU; the register budget keeps the walk there)
+template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false>
+__global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
-    double damping, double2 *__restrict__ ep_part) {
+    double damping, double2 *__restrict__ ep_part, const uint8_t *__restrict__ ewalk,
+    const uint16_t *__restrict__ epos) {
   constexpr int NW = kEpiThreads / kWave;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
   static_assert(MW == 1 || MW == 2 || MW == 4, "mask words");
@@ -826,7 +897,48 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
       const int incl = wave_incl_scan_i32(n2);
       const int pre = incl - n2;
       const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
-      for (int x0 = 0; x0 < C;) {
+      bool walked = false;
+      if constexpr (WALK) {
+        if (__builtin_amdgcn_readfirstlane((int)ewalk[gi]) != 0) {
+          // every class run in one window load (k_epi_walk_plan checked that it fits)
+          for (int y = 0; y < C; ++y) {
+            const int n = __builtin_amdgcn_readlane(n2, y);
+            if (n == 0) continue;
+            const double *src = partial + __builtin_amdgcn_readlane(sa, y);
+            double *dst = win + __builtin_amdgcn_readlane(pre, y);
+            for (int o = 0; o < n; o += 2 * kWave)
+              if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+          }
+          const int T = __builtin_amdgcn_readlane(incl, kWave - 1);  // staged slots (even)
+          auto row_slots = [&](int g) {
+            return __builtin_popcount(mw[0][g]) + (MW > 1 ? __builtin_popcount(mw[MW > 1 ? 1 : 0][g]) : 0);
+          };
+          int mine = 0;  // this lane's slots over the group's blocks
+#pragma unroll
+          for (int g = 0; g < G; ++g) mine += row_slots(g);
+          const int nslots = __builtin_amdgcn_readlane(wave_incl_scan_i32(mine), kWave - 1);
+          // the group's u16 positions after the runs, 16 bytes (8 positions) per lane
+          const int nl = (nslots + 7) >> 3;
+          const double *esrc = reinterpret_cast<const double *>(epos + (size_t)gi * W);
+          for (int o = 0; o < nl; o += kWave)
+            if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + T + 2 * o, 16, 0, 0);
+          __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
+          const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + T);
+          int acc = 0;  // row-major index of block g's first slot
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const int pc = row_slots(g);
+            const int inc = wave_incl_scan_i32(pc);
+            const uint16_t *e = ep + acc + inc - pc;  // this row's slot positions, in class order
+            acc += __builtin_amdgcn_readlane(inc, kWave - 1);
+            for (int k = 0; __ballot(k < pc) != 0ull; ++k)
+              if (k < pc) S[g] = __dadd_rn(S[g], win[e[k]]);
+          }
+          __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+          walked = true;
+        }
+      }
+      for (int x0 = 0; x0 < C && !walked;) {
         const int base = __builtin_amdgcn_readlane(pre, x0);
         const unsigned long long over = __ballot(lane >= x0 && lane < C && incl - base > W);
         const int x1 = over ? (int)__builtin_ctzll(over) : C;  // > x0: one run always fits
@@ -905,12 +1017,82 @@ __global__ __launch_bounds__(kEpiThreads) void k_epilogue_grp(
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
-// k_epilogue_grp instantiations by variant (pr_internal.h kEpiVariants)
+// Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks: the
+// group walks when its class runs (staged exactly as k_epilogue_grp stages them) and its u16
+// slot positions fit one window; then epos[group][k] = window position of the group's k-th slot
+// in row-major order (row, then class), the index epi_class_add would compute for it.
+template <int C, int G, int W>
+__global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, const void *__restrict__ rmask_v,
+                                                               const int32_t *__restrict__ cbase,
+                                                               uint8_t *__restrict__ ewalk,
+                                                               uint16_t *__restrict__ epos) {
+  static_assert(C <= kWave, "per-row walk: at most 64 classes");
+  constexpr int MW = mask_words<C>();
+  const int lane = lane_id();
+  const int64_t ngrp = (nblk + G - 1) / G;
+  const int64_t nw = (int64_t)gridDim.x * (kEpiThreads / kWave);
+  for (int64_t gi = (int64_t)blockIdx.x * (kEpiThreads / kWave) + wave_id(); gi < ngrp; gi += nw) {
+    const int64_t b0 = gi * G;
+    const int nb = (int)min((int64_t)G, nblk - b0);
+    uint64_t m[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t L = (b0 + g) * kWave + lane;
+      if (g >= nb) m[g] = 0;
+      else if constexpr (MW == 2) m[g] = static_cast<const uint64_t *>(rmask_v)[L];
+      else m[g] = static_cast<const uint32_t *>(rmask_v)[L];
+    }
+    const int cs = lane < C ? cbase[b0 * C + lane] : 0;
+    const int ce = lane < C ? cbase[(b0 + nb) * C + lane] : 0;
+    const int sa = cs & ~1;
+    const int n2 = (lane < C && ce > cs) ? (((ce + 1) & ~1) - sa) : 0;
+    const int incl = wave_incl_scan_i32(n2);
+    const int roff = incl - n2 + (cs - sa);
+    const int T = __builtin_amdgcn_readlane(incl, kWave - 1);
+    int pref[G], acc = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int pc = __popcll(m[g]);
+      const int inc = wave_incl_scan_i32(pc);
+      pref[g] = acc + inc - pc;
+      acc += __builtin_amdgcn_readlane(inc, kWave - 1);
+    }
+    const bool walk = acc <= W && T + 2 * ((acc + 7) >> 3) <= W;
+    if (lane == 0) ewalk[gi] = walk ? 1 : 0;
+    if (!walk) continue;
+    uint16_t *out = epos + (size_t)gi * W;
+    for (int x = 0; x < C; ++x) {
+      int run = __builtin_amdgcn_readlane(roff, x);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const bool has = (m[g] >> x) & 1ull;
+        const unsigned long long bal = __ballot(has);
+        if (has) {
+          const int k = __popcll(m[g] & ((1ull << x) - 1ull));  // classes of the row before x
+          const int idx = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)run));
+          out[pref[g] + k] = (uint16_t)idx;
+        }
+        run += __popcll(bal);
+      }
+    }
+  }
+}
+
+// k_epilogue_grp instantiations by variant (pr_internal.h kEpiVariants); walk: the per-row walk
+// of sparse groups (variants 0 and 7, at most 64 classes)
 using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
-                          double *, const double *, SlotPos, double, double, double, double2 *);
+                          double *, const double *, SlotPos, double, double, double, double2 *, const uint8_t *,
+                          const uint16_t *);
+inline bool epi_walk_variant(int C, int var) { return C <= kWave && (var == 0 || var == 7); }
 template <int C>
-inline EpiGrpFn epi_grp_kernel_c(int var) {
+inline EpiGrpFn epi_grp_kernel_c(int var, bool walk) {
+  if constexpr (C <= kWave) {
+    if (walk && var == 7) return k_epilogue_grp<C, kEpiVariants[7].G, kEpiVariants[7].W, false, true>;
+    if (walk && var == 0) return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W, false, true>;
+  }
   switch (var) {
+    case 7: return k_epilogue_grp<C, kEpiVariants[7].G, kEpiVariants[7].W>;
     case 1: return k_epilogue_grp<C, kEpiVariants[1].G, kEpiVariants[1].W>;
     case 2: return k_epilogue_grp<C, kEpiVariants[2].G, kEpiVariants[2].W>;
     case 3: return k_epilogue_grp<C, kEpiVariants[3].G, kEpiVariants[3].W>;
@@ -920,10 +1102,11 @@ inline EpiGrpFn epi_grp_kernel_c(int var) {
     default: return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W>;
   }
 }
-inline EpiGrpFn epi_grp_kernel(int C, int var) {
-  if (C == 128) return epi_grp_kernel_c<128>(var);
-  return C == 64 ? epi_grp_kernel_c<64>(var)
-                 : (C == 32 ? epi_grp_kernel_c<32>(var) : (C == 16 ? epi_grp_kernel_c<16>(var) : epi_grp_kernel_c<8>(var)));
+inline EpiGrpFn epi_grp_kernel(int C, int var, bool walk = false) {
+  if (C == 128) return epi_grp_kernel_c<128>(var, false);
+  return C == 64 ? epi_grp_kernel_c<64>(var, walk)
+                 : (C == 32 ? epi_grp_kernel_c<32>(var, walk)
+                            : (C == 16 ? epi_grp_kernel_c<16>(var, walk) : epi_grp_kernel_c<8>(var, walk)));
 }
 inline size_t epi_grp_lds(int var) { return sizeof(double) * (size_t)(kEpiThreads / kWave) * (kEpiVariants[var].W + 4); }
 

@@ -180,7 +180,12 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // partial-store instructions for every unit (out-of-range ones for unused passes); 24 = the
 // phased kernel (ORDER 0) recording per-workgroup phase clocks (prd_clock_read); 25 = phased
 // with the gathers of unit i + 1 issued before the reduce of unit i (ORDER 0, the product until
-// round 2; 16 is the product, ORDER 1; 17..24 keep ORDER 0).
+// round 2; 16 is the product, ORDER 1; 17..24 keep ORDER 0); ORDER 1 + phased: 26 = no partial
+// stores, 27 = every partial store into one 256 KiB window, 28 = every value from LDS, 29 = partial
+// stores of two slots per lane (16 bytes), 30 = ORDER 3 (the unit's last staged stores issued after
+// the next unit's gathers), 31 / 32 = the carry added through the staging window (one add per
+// lane instead of one per entry; 32 with unconditional window writes); 29 = the product since the
+// 16-byte partial stores (round 3), 33 = the 8-byte partial stores before them.
 // variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 // Copies n workgroups' clocks of the last DIAG 24 launch (17 per workgroup, 100 MHz ticks).
@@ -194,9 +199,20 @@ int prd_clock_read(unsigned long long *out, int n) {
 // contribution buffer from the current one, like an iteration's epilogue; pr_reset afterwards).
 int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
   if (g->C == 1 || !g->epi_grp) return fail(PR_ERR_STATE, "graph has no grouped epilogue");
-  if (variant < 0 || variant >= kNumEpiVariants) return fail(PR_ERR_INVALID, "unknown epilogue variant");
   PR_HIP(hipSetDevice(g->device));
-  const EpiGrpFn epi = epi_grp_kernel(g->C, variant);
+  // variant + 100: the same variant with the per-row walk of sparse groups, planned here for it
+  const bool walk = variant >= 100;
+  variant %= 100;
+  if (variant < 0 || variant >= kNumEpiVariants) return fail(PR_ERR_INVALID, "unknown epilogue variant");
+  if (walk) {
+    const int keep = g->epi_var;
+    g->epi_var = variant;
+    const int rc = plan_epi_walk(g);
+    g->epi_var = keep;
+    if (rc != PR_OK) return rc;
+    if (!g->epi_walk) return fail(PR_ERR_INVALID, "no per-row walk for this variant / class count");
+  }
+  const EpiGrpFn epi = epi_grp_kernel(g->C, variant, walk);
   const size_t lds = epi_grp_lds(variant);
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int G = kEpiVariants[variant].G;
@@ -212,7 +228,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
     hipLaunchKernelGGL(epi, dim3(blocks), dim3(kEpiThreads), lds, g->stream, g->nblk, g->partial.as<double>(),
                        g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
                        g->cbuf[out].as<double>() + g->own_off, g->cbuf[in].as<double>(), g->slots, (double)g->V,
-                       g->teleport, g->damping, part.as<double2>());
+                       g->teleport, g->damping, part.as<double2>(), g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
   PR_HIP(hipGetLastError());
   PR_HIP(hipEventRecord(b, g->stream));
   PR_HIP(hipEventSynchronize(b));
@@ -227,7 +243,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[26] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[34] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -252,12 +268,20 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 4, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 23, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 24, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>)};
+                               reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 2, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 30, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 1, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 31, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<3, 0, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 32, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 33, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 34, 1>)};
   // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
   // (HotGeom.assign); a plain variant keeps the graph's own
   const int assign = variant / 100 - 1;
   variant %= 100;
-  if (variant < 0 || variant > 25 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 33 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
