@@ -525,7 +525,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     }
     // two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an odd
     // last slot alone: half the store instructions of one 8-byte store per slot (-1.7 % at s26,
-    // profiles/r03/; DIAG 34 keeps the 8-byte stores for A/B)
+    // profiles/r02/store_walk/; DIAG 34 keeps the 8-byte stores for A/B)
     if constexpr (!(DIAG == 2 || DIAG == 3 || DIAG == 30 || DIAG == 34)) {
       static_assert(kStageSlots <= 2 * kWave, "one b128 pass");
       const int i2 = 2 * lane_id();
