@@ -407,6 +407,25 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
   }
 }
 
+// ORDER 4: the gather-space half of every entry's value (range-checked buffer loads) is issued a
+// step ahead and nothing waits for it then; the LDS half is read and added when the unit is
+// reduced (wave_unit_add_hot).
+__device__ __forceinline__ void wave_unit_gather_glob(const WaveCodes &w, __amdgpu_buffer_rsrc_t crs,
+                                                      double (&b)[kWavePT]) {
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j)
+    b[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, (w.c[j] & ~1u) ^ kEntGlobal, 0, 0));
+}
+__device__ __forceinline__ void wave_unit_add_hot(const WaveCodes &w, const double *hot, const double (&b)[kWavePT],
+                                                  double (&v)[kWavePT]) {
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) {
+    const uint32_t c = w.c[j] & ~1u;
+    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + ((int32_t)c < 0 ? 0u : c));
+    v[j] = __dadd_rn(a, b[j]);
+  }
+}
+
 // The stores of one staged pass: slots [base, base + n) of the unit from the wave's window.
 template <int DIAG>
 __device__ __forceinline__ void store_staged(const Unit &u, __amdgpu_buffer_rsrc_t prs, const double *stage, int base,
@@ -613,6 +632,28 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   wave_unit_codes<MIK>(u[0], colh, hmeta, k, wc[0]);
   u[1] = unit_at(k1 < end ? k1 : none_k);
   wave_unit_codes<MIK>(u[1], colh, hmeta, k1, wc[1]);
+  if constexpr (ORDER == 4) {
+    // the gathers of unit i + 1 stay in flight while unit i is reduced: their values are added
+    // (LDS half + buffer half) only when that unit is reduced, one step later
+    double vb[3][kWavePT];
+    wave_unit_gather_glob(wc[0], crs, vb[0]);
+    while (true) {
+#pragma unroll
+      for (int sl = 0; sl < 3; ++sl) {
+        const int s1 = (sl + 1) % 3, s2 = (sl + 2) % 3;
+        const int64_t k2 = dyn ? take() : k1 + stride;
+        u[s2] = unit_at(k2 < end ? k2 : none_k);
+        wave_unit_codes<MIK>(u[s2], colh, hmeta, k2, wc[s2]);
+        wave_unit_gather_glob(wc[s1], crs, vb[s1]);
+        double vv[kWavePT];
+        wave_unit_add_hot(wc[sl], hot, vb[sl], vv);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], vv, prs, piece_part, stage);
+        k = k1;
+        k1 = k2;
+        if (k >= end) return;
+      }
+    }
+  }
   wave_unit_gather<DIAG>(wc[0], hot, crs, v[0]);
   while (true) {
 #pragma unroll
@@ -833,7 +874,9 @@ __device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t b
 // has classes instead of C (R-MAT s26: most rows have one or two) -- and the sums are bitwise
 // those of the class loop (the loop's absent classes add an exact +0).
 // (4 waves per SIMD: the LDS of four workgroups per CU; the register budget keeps the walk there)
-template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false>
+// EDIAG (diagnostics library only; results wrong when != 0): 1 = no partial-run DMA (the window
+// is read as it is), 2 = DMA but no per-class adds, 3 = neither (row data, masks, writes only).
+template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false, int EDIAG = 0>
 __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
@@ -942,7 +985,7 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
         const int base = __builtin_amdgcn_readlane(pre, x0);
         const unsigned long long over = __ballot(lane >= x0 && lane < C && incl - base > W);
         const int x1 = over ? (int)__builtin_ctzll(over) : C;  // > x0: one run always fits
-        for (int y = x0; y < x1; ++y) {
+        for (int y = x0; y < x1 && EDIAG != 1 && EDIAG != 3; ++y) {
           const int n = __builtin_amdgcn_readlane(n2, y);
           if (n == 0) continue;
           const double *src = partial + __builtin_amdgcn_readlane(sa, y);
@@ -951,7 +994,7 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
             if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
         }
         __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
-        for (int y = x0; y < x1; ++y) {
+        for (int y = x0; y < x1 && EDIAG < 2; ++y) {
           if (__builtin_amdgcn_readlane(n2, y) == 0) continue;
           const uint32_t bit = 1u << (y & 31);
           const int run = __builtin_amdgcn_readlane(roff, y) - base;

@@ -185,7 +185,8 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // stores of two slots per lane (16 bytes), 30 = ORDER 3 (the unit's last staged stores issued after
 // the next unit's gathers), 31 / 32 = the carry added through the staging window (one add per
 // lane instead of one per entry; 32 with unconditional window writes); 29 = the product since the
-// 16-byte partial stores (round 3), 33 = the 8-byte partial stores before them.
+// 16-byte partial stores (round 2), 33 = the 8-byte partial stores before them, 34 = ORDER 4
+// (the gathers of unit i + 1 in flight while unit i is reduced; adds deferred to the reduce).
 // variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 // Copies n workgroups' clocks of the last DIAG 24 launch (17 per workgroup, 100 MHz ticks).
@@ -200,6 +201,8 @@ int prd_clock_read(unsigned long long *out, int n) {
 int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
   if (g->C == 1 || !g->epi_grp) return fail(PR_ERR_STATE, "graph has no grouped epilogue");
   PR_HIP(hipSetDevice(g->device));
+  const int edv = variant >= 200 ? variant / 100 - 1 : 0;
+  if (edv > 0) variant = 0;
   // variant + 100: the same variant with the per-row walk of sparse groups, planned here for it
   const bool walk = variant >= 100;
   variant %= 100;
@@ -212,7 +215,16 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
     if (rc != PR_OK) return rc;
     if (!g->epi_walk) return fail(PR_ERR_INVALID, "no per-row walk for this variant / class count");
   }
-  const EpiGrpFn epi = epi_grp_kernel(g->C, variant, walk);
+  EpiGrpFn epi = epi_grp_kernel(g->C, variant, walk);
+  // variant 200 / 300 / 400 (64 classes): variant 0 with k_epilogue_grp EDIAG 1 / 2 / 3
+  if (edv > 0) {
+    if (g->C != 64) return fail(PR_ERR_INVALID, "EDIAG variants need 64 classes");
+    epi = edv == 1 ? k_epilogue_grp<64, kEpiGroup, kEpiWin, false, false, 1>
+                   : (edv == 2 ? k_epilogue_grp<64, kEpiGroup, kEpiWin, false, false, 2>
+                               : k_epilogue_grp<64, kEpiGroup, kEpiWin, false, false, 3>);
+    PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)epi_grp_lds(0)));
+  }
   const size_t lds = epi_grp_lds(variant);
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int G = kEpiVariants[variant].G;
@@ -243,7 +255,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[34] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[35] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -276,12 +288,13 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<3, 0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 32, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 33, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<1, 34, 1>)};
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 34, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<4, 0, 1>)};
   // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
   // (HotGeom.assign); a plain variant keeps the graph's own
   const int assign = variant / 100 - 1;
   variant %= 100;
-  if (variant < 0 || variant > 33 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 34 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
