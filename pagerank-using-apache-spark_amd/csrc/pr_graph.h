@@ -74,11 +74,11 @@ struct pr_graph {
   bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
   bool epi_grp = false;     // epi_abs + a sentinel cbase row: k_epilogue_grp (LDS-staged class runs)
   int epi_var = 0;          // its (group, window) variant, pr_spmv.h kEpiVariants (PR_EPI_VAR)
-  // per-row walk of sparse groups in k_epilogue_grp (PR_EPI_WALK): per group a flag (ewalk, u8)
-  // and, for walking groups, every slot's window position in row-major order (epos, u16 [group][W])
+  // per-row walk in k_epilogue_grp (PR_EPI_WALK): per group the first of its u16 slot positions
+  // in epos, or -1 for the class loop (eoff, i64)
   bool epi_walk = false;
   int64_t n_walk_groups = 0;
-  pr::DevBuf ewalk, epos;
+  pr::DevBuf eoff, epos;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
   pr::DevBuf cbuf[2];

@@ -165,39 +165,58 @@ int prepare_hot_kernel() {
   return PR_OK;
 }
 
-// The per-row walk of sparse epilogue groups (pr_spmv.h k_epilogue_grp WALK): on by default for
-// the grouped epilogue's variants 0 and 7 at <= 64 classes; PR_EPI_WALK=0 keeps the class loop
-// everywhere (A/B).  Plans which groups walk and their slots' window positions.
+// The per-row walk of the grouped epilogue (pr_spmv.h k_epilogue_grp WALK): on by default for its
+// variants 0 and 7 at <= 64 classes for the groups that fit one window load (PR_EPI_WALK=1);
+// 0 keeps the class loop everywhere, 2 walks by the step estimate (A/B, k_epi_walk_plan).  Plans
+// which groups walk (k_epi_walk_plan COUNT), places their positions (host prefix over the groups)
+// and writes them.
 int plan_epi_walk(pr_graph *g) {
   g->epi_walk = false;
   g->n_walk_groups = 0;
-  bool on = true;
-  if (const char *e = getenv("PR_EPI_WALK")) on = atoi(e) != 0;
-  if (!on || !g->epi_grp || !epi_walk_variant(g->C, g->epi_var) || g->nblk <= 0) return PR_OK;
-  const int G = kEpiVariants[g->epi_var].G, W = kEpiVariants[g->epi_var].W;
+  int rule = 1;
+  if (const char *e = getenv("PR_EPI_WALK")) rule = std::min(std::max(atoi(e), 0), 2);
+  if (rule == 0 || !g->epi_grp || !epi_walk_variant(g->C, g->epi_var) || g->nblk <= 0) return PR_OK;
+  const int G = kEpiVariants[g->epi_var].G;
   const int64_t ngrp = (g->nblk + G - 1) / G;
-  PR_TRY(g->ewalk.alloc((size_t)ngrp));
-  PR_TRY(g->epos.alloc(sizeof(uint16_t) * (size_t)ngrp * W));
-  const unsigned blocks = grid_for(ngrp, kEpiThreads / kWave, 8192);
-  using PlanFn = void (*)(int64_t, const void *, const int32_t *, uint8_t *, uint16_t *);
-  PlanFn fn = nullptr;
+  using PlanFn = void (*)(int64_t, const void *, const int32_t *, int64_t *, uint16_t *, int);
+  PlanFn count = nullptr, write = nullptr;
+  constexpr int G7 = kEpiVariants[7].G, W7 = kEpiVariants[7].W;
+  static_assert(kEpiVariants[0].G == kEpiGroup && kEpiVariants[0].W == kEpiWin, "variant 0 is the default");
   const bool wide = g->epi_var == 7;
+#define PR_WALK_PLAN(CC)                                                                                   \
+  count = wide ? k_epi_walk_plan<CC, G7, W7, true> : k_epi_walk_plan<CC, kEpiGroup, kEpiWin, true>;        \
+  write = wide ? k_epi_walk_plan<CC, G7, W7, false> : k_epi_walk_plan<CC, kEpiGroup, kEpiWin, false>;
   switch (g->C) {
-    case 8: fn = wide ? k_epi_walk_plan<8, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<8, kEpiGroup, kEpiWin>; break;
-    case 16: fn = wide ? k_epi_walk_plan<16, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<16, kEpiGroup, kEpiWin>; break;
-    case 32: fn = wide ? k_epi_walk_plan<32, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<32, kEpiGroup, kEpiWin>; break;
-    case 64: fn = wide ? k_epi_walk_plan<64, kEpiVariants[7].G, kEpiVariants[7].W> : k_epi_walk_plan<64, kEpiGroup, kEpiWin>; break;
+    case 8: PR_WALK_PLAN(8) break;
+    case 16: PR_WALK_PLAN(16) break;
+    case 32: PR_WALK_PLAN(32) break;
+    case 64: PR_WALK_PLAN(64) break;
     default: return PR_OK;
   }
-  static_assert(kEpiVariants[0].G == kEpiGroup && kEpiVariants[0].W == kEpiWin, "variant 0 is the default");
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p, g->cbase.as<int32_t>(),
-                     g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
+#undef PR_WALK_PLAN
+  PR_TRY(g->eoff.alloc(sizeof(int64_t) * (size_t)ngrp));
+  const unsigned blocks = grid_for(ngrp, kEpiThreads / kWave, 8192);
+  hipLaunchKernelGGL(count, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p, g->cbase.as<int32_t>(),
+                     g->eoff.as<int64_t>(), nullptr, rule);
   PR_HIP(hipGetLastError());
-  std::vector<uint8_t> flags((size_t)ngrp);
-  PR_HIP(hipMemcpyAsync(flags.data(), g->ewalk.p, (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
+  std::vector<int64_t> off((size_t)ngrp);
+  PR_HIP(hipMemcpyAsync(off.data(), g->eoff.p, sizeof(int64_t) * (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
-  g->n_walk_groups = 0;
-  for (uint8_t f : flags) g->n_walk_groups += f;
+  int64_t total = 0;
+  for (auto &o : off) {
+    if (o < 0) continue;
+    const int64_t n = o;
+    o = total;  // a multiple of 8 positions: every batch's run of positions is padded to 16 bytes
+    total += n;
+    ++g->n_walk_groups;
+  }
+  PR_TRY(g->epos.alloc(sizeof(uint16_t) * (size_t)(total > 0 ? total : 8)));
+  PR_HIP(hipMemcpyAsync(g->eoff.p, off.data(), sizeof(int64_t) * (size_t)ngrp, hipMemcpyHostToDevice, g->stream));
+  if (total > 0)
+    hipLaunchKernelGGL(write, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p,
+                       g->cbase.as<int32_t>(), g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), rule);
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipStreamSynchronize(g->stream));
   g->epi_walk = true;
   return PR_OK;
 }
@@ -322,7 +341,7 @@ int iter_compute(pr_graph *g) {
                          g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                          g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                          (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
-                         g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
+                         g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
     } else {
     auto *epi = g->epi_abs ? (g->C == 32 ? k_epilogue<32, true> : (g->C == 16 ? k_epilogue<16, true> : k_epilogue<8, true>))
                            : (g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>));

@@ -867,13 +867,33 @@ __device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t b
 // even slots (16-byte alignment): slot s of a run staged at window offset f sits at
 // f + s - (s & ~1).  Each wave's window is W slots plus a zero slot (and one of padding).
 //
-// WALK (per-row walk of sparse groups, PR_EPI_WALK): a group the build marked in ewalk has all of
-// its class runs in one window load, followed in the window by the u16 window positions of its
-// slots in row-major order (epos, planned by k_epi_walk_plan with the same staging rules).  Each
-// row then adds only its own slots, in class order -- as many steps as the block's busiest row
-// has classes instead of C (R-MAT s26: most rows have one or two) -- and the sums are bitwise
-// those of the class loop (the loop's absent classes add an exact +0).
+// WALK (per-row walk, PR_EPI_WALK): for a group the build chose (eoff[group] >= 0: where the
+// walk is the cheaper of the two), each batch of classes holds the staged runs followed in the
+// window by the u16 window positions of the batch's slots (epos, row-major: block, row, class),
+// batched so that both fit (walk_batch_end).  Each row then adds only its own slots, in class
+// order -- as many steps per batch and block as its busiest row has classes there, instead of
+// one per class -- and the sums are bitwise those of the class loop (whose absent classes add an
+// exact +0).  k_epi_walk_plan plans the positions with the same staging and batching rules.
 // (4 waves per SIMD: the LDS of four workgroups per CU; the register budget keeps the walk there)
+// The walk's batches (k_epilogue_grp WALK, k_epi_walk_plan): from class x0, the longest run of
+// classes whose staged runs plus their slots' u16 positions (in 16-byte lanes) fit the window.
+// Lane y holds class y's run prefix (incl, pre) and slot-count prefix (sincl, spre).  One class
+// always fits: at most 64 G + 2 staged slots and 64 G positions (<= 8 G + 2 more slots) <= W.
+template <int C, int W>
+__device__ __forceinline__ int walk_batch_end(int x0, int incl, int pre, int sincl, int spre) {
+  static_assert(W >= 64 * kEpiGroup + 2 + 2 * 8 * kEpiGroup, "one class and its positions fit the window");
+  const int lane = lane_id();
+  const int base = __builtin_amdgcn_readlane(pre, x0), sbase = __builtin_amdgcn_readlane(spre, x0);
+  const int need = (incl - base) + 2 * ((sincl - sbase + 7) >> 3);
+  const unsigned long long over = __ballot(lane >= x0 && lane < C && need > W);
+  return over ? (int)__builtin_ctzll(over) : C;
+}
+// bits [x0, x1) of a 64-bit class mask
+__device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
+  const uint64_t hi = x1 >= 64 ? ~0ull : ((1ull << x1) - 1ull);
+  return hi & ~((1ull << x0) - 1ull);
+}
+
 // EDIAG (diagnostics library only; results wrong when != 0): 1 = no partial-run DMA (the window
 // is read as it is), 2 = DMA but no per-class adds, 3 = neither (row data, masks, writes only).
 template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false, int EDIAG = 0>
@@ -881,7 +901,7 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
-    double damping, double2 *__restrict__ ep_part, const uint8_t *__restrict__ ewalk,
+    double damping, double2 *__restrict__ ep_part, const int64_t *__restrict__ eoff,
     const uint16_t *__restrict__ epos) {
   constexpr int NW = kEpiThreads / kWave;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
@@ -942,42 +962,47 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
       const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
       bool walked = false;
       if constexpr (WALK) {
-        if (__builtin_amdgcn_readfirstlane((int)ewalk[gi]) != 0) {
-          // every class run in one window load (k_epi_walk_plan checked that it fits)
-          for (int y = 0; y < C; ++y) {
-            const int n = __builtin_amdgcn_readlane(n2, y);
-            if (n == 0) continue;
-            const double *src = partial + __builtin_amdgcn_readlane(sa, y);
-            double *dst = win + __builtin_amdgcn_readlane(pre, y);
-            for (int o = 0; o < n; o += 2 * kWave)
-              if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
-          }
-          const int T = __builtin_amdgcn_readlane(incl, kWave - 1);  // staged slots (even)
-          auto row_slots = [&](int g) {
-            return __builtin_popcount(mw[0][g]) + (MW > 1 ? __builtin_popcount(mw[MW > 1 ? 1 : 0][g]) : 0);
-          };
-          int mine = 0;  // this lane's slots over the group's blocks
+        const int64_t eo = eoff[gi];
+        if (eo >= 0) {
+          const int nsl = lane < C ? ce - cs : 0;  // class y's slots in this group
+          const int sincl = wave_incl_scan_i32(nsl);
+          const int spre = sincl - nsl;
+          int64_t ebase = eo;  // the batch's first position entry (16-byte aligned)
+          for (int x0 = 0; x0 < C;) {
+            const int x1 = walk_batch_end<C, W>(x0, incl, pre, sincl, spre);
+            const int base = __builtin_amdgcn_readlane(pre, x0);
+            const int sbase = __builtin_amdgcn_readlane(spre, x0);
+            for (int y = x0; y < x1; ++y) {
+              const int n = __builtin_amdgcn_readlane(n2, y);
+              if (n == 0) continue;
+              const double *src = partial + __builtin_amdgcn_readlane(sa, y);
+              double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
+              for (int o = 0; o < n; o += 2 * kWave)
+                if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+            }
+            const int Tb = __builtin_amdgcn_readlane(incl, x1 - 1) - base;  // staged slots (even)
+            const int nl = (__builtin_amdgcn_readlane(sincl, x1 - 1) - sbase + 7) >> 3;  // 16-byte lanes
+            const double *esrc = reinterpret_cast<const double *>(epos + ebase);
+            for (int o = 0; o < nl; o += kWave)
+              if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
+            ebase += 8 * nl;
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
+            const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
+            const uint64_t bm = class_range_mask(x0, x1);
+            int acc = 0;  // index of block g's first position in the batch
 #pragma unroll
-          for (int g = 0; g < G; ++g) mine += row_slots(g);
-          const int nslots = __builtin_amdgcn_readlane(wave_incl_scan_i32(mine), kWave - 1);
-          // the group's u16 positions after the runs, 16 bytes (8 positions) per lane
-          const int nl = (nslots + 7) >> 3;
-          const double *esrc = reinterpret_cast<const double *>(epos + (size_t)gi * W);
-          for (int o = 0; o < nl; o += kWave)
-            if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + T + 2 * o, 16, 0, 0);
-          __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
-          const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + T);
-          int acc = 0;  // row-major index of block g's first slot
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            const int pc = row_slots(g);
-            const int inc = wave_incl_scan_i32(pc);
-            const uint16_t *e = ep + acc + inc - pc;  // this row's slot positions, in class order
-            acc += __builtin_amdgcn_readlane(inc, kWave - 1);
-            for (int k = 0; __ballot(k < pc) != 0ull; ++k)
-              if (k < pc) S[g] = __dadd_rn(S[g], win[e[k]]);
+            for (int g = 0; g < G; ++g) {
+              const uint64_t m = ((uint64_t)(MW > 1 ? mw[MW > 1 ? 1 : 0][g] : 0u) << 32 | mw[0][g]) & bm;
+              const int cnt = __popcll(m);
+              const int inc = wave_incl_scan_i32(cnt);
+              const uint16_t *e = ep + acc + inc - cnt;  // this row's positions, in class order
+              acc += __builtin_amdgcn_readlane(inc, kWave - 1);
+              for (int k = 0; __ballot(k < cnt) != 0ull; ++k)
+                if (k < cnt) S[g] = __dadd_rn(S[g], win[e[k]]);
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+            x0 = x1;
           }
-          __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
           walked = true;
         }
       }
@@ -1060,21 +1085,31 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
-// Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks: the
-// group walks when its class runs (staged exactly as k_epilogue_grp stages them) and its u16
-// slot positions fit one window; then epos[group][k] = window position of the group's k-th slot
-// in row-major order (row, then class), the index epi_class_add would compute for it.
-template <int C, int G, int W>
+// Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks, with
+// k_epilogue_grp's staging and the walk's batching.  COUNT: eoff[group] = the group's position
+// entries (16-byte padded per batch) if it walks, else -1.  Rule (PR_EPI_WALK): 1 (default) = the
+// group fits one batch (runs and positions in one window load: the sparse tail of R-MAT); 2 = any
+// group whose walk takes at most 3/4 of the class loop's steps (per batch and block the busiest
+// row's classes, against one per class with slots) -- slower in practice (R-MAT s26 +3 %, ER s24
+// +18 %: a walk step costs more than a loop step, and the positions add 2 B per slot).  !COUNT:
+// for every group with eoff >= 0, the window position of each slot (the index epi_class_add would
+// compute) at epos[eoff + ...].
+template <int C, int G, int W, bool COUNT>
 __global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, const void *__restrict__ rmask_v,
                                                                const int32_t *__restrict__ cbase,
-                                                               uint8_t *__restrict__ ewalk,
-                                                               uint16_t *__restrict__ epos) {
+                                                               int64_t *__restrict__ eoff,
+                                                               uint16_t *__restrict__ epos, int rule) {
   static_assert(C <= kWave, "per-row walk: at most 64 classes");
   constexpr int MW = mask_words<C>();
   const int lane = lane_id();
   const int64_t ngrp = (nblk + G - 1) / G;
   const int64_t nw = (int64_t)gridDim.x * (kEpiThreads / kWave);
   for (int64_t gi = (int64_t)blockIdx.x * (kEpiThreads / kWave) + wave_id(); gi < ngrp; gi += nw) {
+    int64_t ebase = 0;
+    if constexpr (!COUNT) {
+      ebase = eoff[gi];
+      if (ebase < 0) continue;
+    }
     const int64_t b0 = gi * G;
     const int nb = (int)min((int64_t)G, nblk - b0);
     uint64_t m[G];
@@ -1090,42 +1125,67 @@ __global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, con
     const int sa = cs & ~1;
     const int n2 = (lane < C && ce > cs) ? (((ce + 1) & ~1) - sa) : 0;
     const int incl = wave_incl_scan_i32(n2);
-    const int roff = incl - n2 + (cs - sa);
-    const int T = __builtin_amdgcn_readlane(incl, kWave - 1);
-    int pref[G], acc = 0;
+    const int pre = incl - n2;
+    const int roff = pre + (cs - sa);
+    const int nsl = lane < C ? ce - cs : 0;
+    const int sincl = wave_incl_scan_i32(nsl);
+    const int spre = sincl - nsl;
+    int64_t loop_steps = 0, walk_steps = 0, total = 0;
+    int batches = 0;
+    for (int x0 = 0; x0 < C;) {
+      const int x1 = walk_batch_end<C, W>(x0, incl, pre, sincl, spre);
+      const int base = __builtin_amdgcn_readlane(pre, x0), sbase = __builtin_amdgcn_readlane(spre, x0);
+      const int nl = (__builtin_amdgcn_readlane(sincl, x1 - 1) - sbase + 7) >> 3;
+      const uint64_t bm = class_range_mask(x0, x1);
+      if constexpr (COUNT) {
+        loop_steps += (int64_t)G * __popcll(__ballot(lane >= x0 && lane < x1 && n2 > 0));
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int pc = __popcll(m[g]);
-      const int inc = wave_incl_scan_i32(pc);
-      pref[g] = acc + inc - pc;
-      acc += __builtin_amdgcn_readlane(inc, kWave - 1);
-    }
-    const bool walk = acc <= W && T + 2 * ((acc + 7) >> 3) <= W;
-    if (lane == 0) ewalk[gi] = walk ? 1 : 0;
-    if (!walk) continue;
-    uint16_t *out = epos + (size_t)gi * W;
-    for (int x = 0; x < C; ++x) {
-      int run = __builtin_amdgcn_readlane(roff, x);
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const bool has = (m[g] >> x) & 1ull;
-        const unsigned long long bal = __ballot(has);
-        if (has) {
-          const int k = __popcll(m[g] & ((1ull << x) - 1ull));  // classes of the row before x
-          const int idx = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)run));
-          out[pref[g] + k] = (uint16_t)idx;
+        for (int g = 0; g < G; ++g) {
+          int c = __popcll(m[g] & bm);
+          for (int off = kWave / 2; off > 0; off >>= 1) c = max(c, __shfl_xor(c, off, kWave));
+          walk_steps += c;
         }
-        run += __popcll(bal);
+        total += 8 * nl;
+        ++batches;
+      } else {
+        int pref[G], acc = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int cnt = __popcll(m[g] & bm);
+          const int inc = wave_incl_scan_i32(cnt);
+          pref[g] = acc + inc - cnt;
+          acc += __builtin_amdgcn_readlane(inc, kWave - 1);
+        }
+        for (int x = x0; x < x1; ++x) {
+          int run = __builtin_amdgcn_readlane(roff, x) - base;
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const bool has = (m[g] >> x) & 1ull;
+            const unsigned long long bal = __ballot(has);
+            if (has) {
+              const int k = __popcll(m[g] & bm & ((1ull << x) - 1ull));  // the row's classes before x in the batch
+              epos[ebase + pref[g] + k] = (uint16_t)__builtin_amdgcn_mbcnt_hi(
+                  (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)run));
+            }
+            run += __popcll(bal);
+          }
+        }
+        ebase += 8 * nl;
       }
+      x0 = x1;
     }
+    if constexpr (COUNT)
+      if (lane == 0) {
+        const bool walk = rule == 1 ? batches == 1 : walk_steps * 4 <= loop_steps * 3;
+        eoff[gi] = walk ? total : -1;
+      }
   }
 }
 
 // k_epilogue_grp instantiations by variant (pr_internal.h kEpiVariants); walk: the per-row walk
 // of sparse groups (variants 0 and 7, at most 64 classes)
 using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
-                          double *, const double *, SlotPos, double, double, double, double2 *, const uint8_t *,
+                          double *, const double *, SlotPos, double, double, double, double2 *, const int64_t *,
                           const uint16_t *);
 inline bool epi_walk_variant(int C, int var) { return C <= kWave && (var == 0 || var == 7); }
 template <int C>

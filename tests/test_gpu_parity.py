@@ -571,34 +571,37 @@ def test_epilogue_staging_modes_bitwise(hip, oracle_c, monkeypatch):
 
 @pytest.mark.parametrize("classes,var", [("64", "0"), ("32", "0"), ("16", "7"), ("64", "7")])
 def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
-    """k_epilogue_grp walks the rows of sparse groups over their own slots (PR_EPI_WALK, the
-    default) instead of looping over every class: the same slots added in the same class order,
-    so the ranks are bitwise those of the class loop (PR_EPI_WALK=0), for dense hubs and sparse
-    tails alike, and within the bar of the oracle (Sparky.java:229-233)."""
+    """k_epilogue_grp walks the rows of sparse groups over their own slots (PR_EPI_WALK=1, the
+    default: groups that fit one window load; 2: by step estimate, multi-batch) instead of looping
+    over every class: the same slots added in the same class order, so the ranks are bitwise
+    those of the class loop (PR_EPI_WALK=0), for dense groups and sparse tails alike, and within
+    the bar of the oracle (Sparky.java:229-233)."""
     monkeypatch.setenv("PR_CLASSES", classes)
     monkeypatch.setenv("PR_HOT_SLOTS", "400")
     monkeypatch.setenv("PR_EPI_VAR", var)
     rng = np.random.default_rng(47)
-    V = 90000
-    # sparse rows (about one in-link each) for walking groups, a block of dense rows and a hub
-    # for class-loop groups and long walks
-    # (3000 rows with ~100 in-links, made the top out-degrees so that they share blocks)
-    src, dst = random_edges(rng, V, 40000, hub_frac=0.02)
-    dense_src = np.concatenate([rng.integers(0, V, 300000), np.repeat(np.arange(3000), 10)]).astype(np.int32)
-    dense_dst = np.concatenate([rng.integers(0, 3000, 300000), rng.integers(0, V, 30000)]).astype(np.int32)
+    C = int(classes)
+    V = max(90000, 1024 * C)
+    # sparse rows (about one in-link each: walking groups) and 512 * C dense rows with ~3 C
+    # in-links each, made the top out-degrees so that they fill whole groups (the class loop is
+    # cheaper there), plus a hub (a long walk)
+    D = 512 * C
+    src, dst = random_edges(rng, V, V // 2, hub_frac=0.02)
+    dense_src = rng.integers(0, D, 3 * C * D).astype(np.int32)
+    dense_dst = rng.integers(0, D, 3 * C * D).astype(np.int32)
     src, dst = np.concatenate([src, dense_src]), np.concatenate([dst, dense_dst])
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 6)
     out = {}
-    for walk in ("1", "0"):
+    for walk in ("1", "2", "0"):  # one-window groups (default), by step estimate, never
         monkeypatch.setenv("PR_EPI_WALK", walk)
         with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
             info = g.info()
             assert info["classes"] == int(classes) and info["epilogue"] == 3
             ngrp = -(-info["local_rows"] // 512)
-            if walk == "1":  # both kinds of group are present
-                assert 0 < info["walk_groups"] < ngrp, (info["walk_groups"], ngrp)
+            if walk != "0":  # both kinds of group are present
+                assert 0 < info["walk_groups"] < ngrp, (walk, info["walk_groups"], ngrp)
             else:
                 assert info["walk_groups"] == 0
             out[walk], _ = g.run(6)
-    assert np.array_equal(out["1"], out["0"])
+    assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL

@@ -240,7 +240,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
     hipLaunchKernelGGL(epi, dim3(blocks), dim3(kEpiThreads), lds, g->stream, g->nblk, g->partial.as<double>(),
                        g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(), g->r.as<double>(),
                        g->cbuf[out].as<double>() + g->own_off, g->cbuf[in].as<double>(), g->slots, (double)g->V,
-                       g->teleport, g->damping, part.as<double2>(), g->ewalk.as<uint8_t>(), g->epos.as<uint16_t>());
+                       g->teleport, g->damping, part.as<double2>(), g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
   PR_HIP(hipGetLastError());
   PR_HIP(hipEventRecord(b, g->stream));
   PR_HIP(hipEventSynchronize(b));
