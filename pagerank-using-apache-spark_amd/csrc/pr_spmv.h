@@ -451,7 +451,21 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
-  const uint32_t meta = MIK ? derive_meta(w) : w.meta;
+  // DIAG 37: when every lane holds a segment end (short segments), the carry into a lane is the
+  // previous lane's tail alone, so the segmented scan and its predicates are skipped (same sums)
+  uint32_t meta;
+  bool all_ends = false;
+  if constexpr (DIAG == 37 && MIK) {
+    uint32_t em = 0;
+#pragma unroll
+    for (int j = 0; j < kWavePT; ++j) em |= (w.c[j] & 1u) << j;
+    all_ends = __ballot(em != 0u) == ~0ull;
+    meta = all_ends ? (em | ((uint32_t)(wave_incl_scan_i32(__builtin_popcount(em)) - __builtin_popcount(em))
+                             << kMetaExclShift))
+                    : derive_meta(w);
+  } else {
+    meta = MIK ? derive_meta(w) : w.meta;
+  }
   const uint32_t endm = meta & 0xFFu;
   double sv[kWavePT];
   double acc = 0.0;
@@ -463,6 +477,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   }
   // segmented inclusive scan of the lane tails; partner-add predicates precomputed
   double a = acc, p;
+  if (all_ends) goto scanned;
   p = dpp_f64<0x111>(a);  // row_shr:1
   if (meta & kMetaStep0) a = __dadd_rn(p, a);
   p = dpp_f64<0x112>(a);  // row_shr:2
@@ -475,6 +490,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   if (meta & (kMetaStep0 << 4)) a = __dadd_rn(p, a);
   p = dpp_f64<0x143>(a);  // row_bcast:31
   if (meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
+scanned:
   const double carry = dpp_f64<0x138>(a);  // wave_shr:1 (lane 0 reads 0)
   // lane's first segment end gets the carry; segment s of the unit is row r0 + s.  The sums are
   // staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced 512-byte
@@ -723,7 +739,22 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
     // loop pays two dependent memory latencies per element, 18 times per phase
     const int32_t *hp = hpos + (int64_t)x * nh;
     constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18430 slots)
-    for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
+    // DIAG 35 (timing only, wrong values): the hot set is staged for the first phase only.
+    // DIAG 36: at P = 1 the class's hot set is rows [x Q_pad, + q_load) of the slice, contiguous:
+    // staged by 4-byte LDS-DMA instead of position loads and gathers through registers.
+    bool staged = DIAG == 35 && ph > p_lo;
+    if constexpr (DIAG == 36) {
+      if (hg.P == 1) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(cin + (int64_t)x * hg.Q_pad);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(hot + 1);
+        const int nd = 2 * hg.q_load, ln = lane_id();
+        for (int b = wv * kWave; b < nd; b += kHotThreads)
+          if (b + ln < nd) __builtin_amdgcn_global_load_lds(src + b + ln, dst + b, 4, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed before the barrier
+        staged = true;
+      }
+    }
+    for (int b0 = 0; b0 < nh && !staged; b0 += kSB * kHotThreads) {
       int32_t pos[kSB];
       double val[kSB];
 #pragma unroll

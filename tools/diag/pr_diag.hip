@@ -186,7 +186,10 @@ int prd_time_spmv(pr_graph *g, int variant, uint32_t mask, int iters, double *ms
 // the next unit's gathers), 31 / 32 = the carry added through the staging window (one add per
 // lane instead of one per entry; 32 with unconditional window writes); 29 = the product since the
 // 16-byte partial stores (round 2), 33 = the 8-byte partial stores before them, 34 = ORDER 4
-// (the gathers of unit i + 1 in flight while unit i is reduced; adds deferred to the reduce).
+// (the gathers of unit i + 1 in flight while unit i is reduced; adds deferred to the reduce), 35 =
+// the hot set staged for the first phase only (the cost of restaging), 36 = P = 1 hot sets staged
+// by LDS-DMA, 37 = no segmented scan in units where every lane holds a segment end; ORDER 1 +
+// phased with DIAG 6 / 10 / 12: 38 = exec-masked gathers, 39 = sc1 gathers, 40 = sc0 gathers.
 // variant + 100 * (a + 1): with the unit assignment PR_HOT_ASSIGN = a.  The hot-set size is a build setting
 // (PR_HOT_SLOTS): A/B it with separate graph builds.
 // Copies n workgroups' clocks of the last DIAG 24 launch (17 per workgroup, 100 MHz ticks).
@@ -255,7 +258,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
 int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *ms_out) {
   (void)mask;
   if (g->C == 1) return fail(PR_ERR_STATE, "graph has the fused layout");
-  static const void *tab[35] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
+  static const void *tab[41] ={reinterpret_cast<const void *>(&k_spmv_hot<0, 0>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 2>),
                                reinterpret_cast<const void *>(&k_spmv_hot<0, 3>),
@@ -289,12 +292,18 @@ int prd_time_split(pr_graph *g, int variant, uint32_t mask, int iters, double *m
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 32, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 33, 1>),
                                reinterpret_cast<const void *>(&k_spmv_hot<1, 34, 1>),
-                               reinterpret_cast<const void *>(&k_spmv_hot<4, 0, 1>)};
+                               reinterpret_cast<const void *>(&k_spmv_hot<4, 0, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 35, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 36, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 37, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 6, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 10, 1>),
+                               reinterpret_cast<const void *>(&k_spmv_hot<1, 12, 1>)};
   // variant + 100 * (a + 1): the same kernel with the unit assignment PR_HOT_ASSIGN = a
   // (HotGeom.assign); a plain variant keeps the graph's own
   const int assign = variant / 100 - 1;
   variant %= 100;
-  if (variant < 0 || variant > 34 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
+  if (variant < 0 || variant > 40 || assign > 3) return fail(PR_ERR_INVALID, "unknown variant");
   PR_HIP(hipSetDevice(g->device));
   const void *kern = tab[variant];
   PR_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
