@@ -43,7 +43,7 @@ void DevBuf::reset() {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes + piece_seg.bytes + seg_cnt.bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
   return b;

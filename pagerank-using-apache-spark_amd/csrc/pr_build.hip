@@ -740,7 +740,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   g->n_units = (int64_t)light_units.size();
   g->n_long = (int64_t)lr_row.size();
   g->n_pieces = pieces;
-  if (C > 1) PR_TRY(setup_seg_fold(g));
   PR_TRY(g->units.alloc(sizeof(Unit) * (light_units.size() + 1)));
   PR_TRY(g->lr_row.alloc(sizeof(int32_t) * (lr_row.size() + 1)));
   PR_TRY(g->lr_p0.alloc(sizeof(int32_t) * (lr_p0.size() + 1)));

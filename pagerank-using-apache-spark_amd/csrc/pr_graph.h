@@ -79,7 +79,6 @@ struct pr_graph {
   bool epi_walk = false;
   int64_t n_walk_groups = 0;
   pr::DevBuf eoff, epos;
-  pr::DevBuf piece_seg, seg_cnt;  // long-segment fold in k_spmv_hot (HotGeom.fold, PR_SEG_FOLD)
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
   pr::DevBuf cbuf[2];
@@ -145,7 +144,6 @@ namespace pr {
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (after rmask/cbase)
-int setup_seg_fold(pr_graph *g);  // long segments summed inside k_spmv_hot (after seg_slot/seg_p0)
 int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);

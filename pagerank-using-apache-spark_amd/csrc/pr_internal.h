@@ -183,13 +183,6 @@ struct HotGeom {
   // with its waves interleaved in it, 3 (the default) = the workgroup's units of mode 0 taken by
   // its waves from an LDS counter (balanced within the workgroup)
   int assign;
-  // long segments summed by their last piece inside k_spmv_hot (PR_SEG_FOLD=1; off by default) instead of
-  // k_seg_reduce: piece -> segment, the segments' first pieces and slots, per-segment arrival
-  // counters (monotonic: the last arrival of a launch sees a multiple of the piece count)
-  int fold;
-  const int32_t *piece_seg, *seg_p0;
-  const int64_t *seg_slot;
-  uint32_t *seg_cnt;
   __host__ __device__ int slots() const { return P * Kp + 1; }
   // slot `slots()` is a control word (the workgroup's unit counter of PR_HOT_ASSIGN=3); the
   // staging windows start 16-byte aligned after it

@@ -221,35 +221,6 @@ int plan_epi_walk(pr_graph *g) {
   return PR_OK;
 }
 
-__global__ void k_piece_seg(int64_t n_segs, const int32_t *__restrict__ seg_p0, int32_t *__restrict__ piece_seg) {
-  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n_segs; q += (int64_t)gridDim.x * blockDim.x)
-    for (int32_t p = seg_p0[q]; p < seg_p0[q + 1]; ++p) piece_seg[p] = (int32_t)q;
-}
-
-// Long segments of the split layout: with PR_SEG_FOLD=1 the wave that sums a segment's last
-// piece sums the segment too (pr_spmv.h piece_done), so k_seg_reduce and its launch drop out of
-// the iteration (the same sums in the same order).  Off by default: LJ -0.9 %, s26 +0.2 %,
-// Twitter +3.1 % (its hubs' 1500-piece sums become one wave's tail; profiles/r02/experiments.md).
-int setup_seg_fold(pr_graph *g) {
-  g->hot.fold = 0;
-  bool on = false;
-  if (const char *e = getenv("PR_SEG_FOLD")) on = atoi(e) != 0;
-  if (!on || g->n_segs <= 0 || g->n_pieces <= 0) return PR_OK;
-  PR_TRY(g->piece_seg.alloc(sizeof(int32_t) * (size_t)g->n_pieces));
-  PR_TRY(g->seg_cnt.alloc(sizeof(uint32_t) * (size_t)g->n_segs));
-  PR_HIP(hipMemsetAsync(g->seg_cnt.p, 0, sizeof(uint32_t) * (size_t)g->n_segs, g->stream));
-  hipLaunchKernelGGL(k_piece_seg, dim3(grid_for(g->n_segs, 256, 4096)), dim3(256), 0, g->stream, g->n_segs,
-                     g->seg_p0.as<int32_t>(), g->piece_seg.as<int32_t>());
-  PR_HIP(hipGetLastError());
-  PR_HIP(hipStreamSynchronize(g->stream));
-  g->hot.piece_seg = g->piece_seg.as<int32_t>();
-  g->hot.seg_p0 = g->seg_p0.as<int32_t>();
-  g->hot.seg_slot = g->seg_slot.as<int64_t>();
-  g->hot.seg_cnt = g->seg_cnt.as<uint32_t>();
-  g->hot.fold = 1;
-  return PR_OK;
-}
-
 int n_hot_phases(const pr_graph *g) { return g->hot_phased ? std::max(1, g->C / kXcds) : 1; }
 
 int set_hot_reserve(pr_graph *g, int per_xcd) {
@@ -359,7 +330,7 @@ int iter_compute(pr_graph *g) {
       PR_TRY(join_exchange(g));
       if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
     }
-    if (g->n_segs > 0 && !g->hot.fold)
+    if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());

@@ -438,50 +438,17 @@ __device__ __forceinline__ void store_staged(const Unit &u, __amdgpu_buffer_rsrc
 
 // DEFER (diagnostics, ORDER 3): the last staged pass is not stored here; *dbase / *dn say which
 // slots the caller stores later (store_staged) -- after the next unit's gathers are issued.
-// A PIECE unit's sum goes to piece_part; with hg.fold the wave that brings the last piece of its
-// segment then sums the segment's pieces in piece order -- exactly as k_seg_reduce would -- into
-// the segment's partial slot (piece sums are written and read at agent scope, past L1).
-__device__ __forceinline__ void piece_done(const HotGeom &hg, int piece, double acc, double *__restrict__ piece_part,
-                                           double *__restrict__ partial) {
-  const int lane = lane_id();
-  if (!hg.fold) {
-    if (lane == 0) piece_part[piece] = acc;
-    return;
-  }
-  int last = 0;
-  if (lane == 0) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(piece_part + piece),
-                       (unsigned long long)__double_as_longlong(acc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int q = hg.piece_seg[piece];
-    const int np = hg.seg_p0[q + 1] - hg.seg_p0[q];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the piece sum is out before it is counted
-    const uint32_t prev = __hip_atomic_fetch_add(hg.seg_cnt + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev + 1u) % (uint32_t)np == 0u ? q + 1 : 0;
-  }
-  last = __builtin_amdgcn_readlane(last, 0);
-  if (last == 0) return;
-  const int q = last - 1, p0 = hg.seg_p0[q], np = hg.seg_p0[q + 1] - p0;
-  double s = 0.0;
-  for (int k = lane; k < np; k += kWave)
-    s = __dadd_rn(s, __longlong_as_double((long long)__hip_atomic_load(
-                         reinterpret_cast<const unsigned long long *>(piece_part + p0 + k), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT)));
-  s = wave_sum(s);
-  if (lane == 0) partial[hg.seg_slot[q]] = s;
-}
-
 template <int DIAG, bool MIK, bool DEFER = false>
 __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
                                                  __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
-                                                 double *stage, const HotGeom &hg, double *__restrict__ partial,
-                                                 int *dbase = nullptr, int *dn = nullptr) {
+                                                 double *stage, int *dbase = nullptr, int *dn = nullptr) {
   if constexpr (DEFER) *dn = 0;
   if (u.meta < 0) {  // PIECE of a long segment
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) acc = __dadd_rn(acc, v[j]);
     acc = wave_sum(acc);
-    piece_done(hg, -u.meta - 1, acc, piece_part, partial);
+    if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
   // DIAG 37: when every lane holds a segment end (short segments), the carry into a lane is the
@@ -696,7 +663,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
         wave_unit_gather_glob(wc[s1], crs, vb[s1]);
         double vv[kWavePT];
         wave_unit_add_hot(wc[sl], hot, vb[sl], vv);
-        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], vv, prs, piece_part, stage, hg, partial);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], vv, prs, piece_part, stage);
         k = k1;
         k1 = k2;
         if (k >= end) return;
@@ -713,14 +680,14 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       wave_unit_codes<MIK>(u[s2], colh, hmeta, k2, wc[s2]);
       if constexpr (ORDER == 0) {
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
-        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage, hg, partial);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
       } else if constexpr (ORDER == 3) {  // diagnostics: the last staged stores after the next gathers
         int db = 0, dn = 0;
-        wave_unit_reduce<DIAG, MIK, true>(u[sl], wc[sl], v[sl], prs, piece_part, stage, hg, partial, &db, &dn);
+        wave_unit_reduce<DIAG, MIK, true>(u[sl], wc[sl], v[sl], prs, piece_part, stage, &db, &dn);
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
         store_staged<DIAG>(u[sl], prs, stage, db, dn);
       } else {  // reduce first: a gather issue stalled by a busy address unit cannot hold it up
-        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage, hg, partial);
+        wave_unit_reduce<DIAG, MIK>(u[sl], wc[sl], v[sl], prs, piece_part, stage);
         wave_unit_gather<DIAG>(wc[s1], hot, crs, v[s1]);
       }
       k = k1;

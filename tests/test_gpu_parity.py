@@ -605,33 +605,3 @@ def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
             out[walk], _ = g.run(6)
     assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
-
-
-@pytest.mark.parametrize("classes", ["64", "8"])
-def test_long_segment_fold_bitwise(hip, oracle_c, monkeypatch, classes):
-    """Long (row, class) segments are split into pieces; with PR_SEG_FOLD=1 the wave that sums a
-    segment's last piece also sums the segment, in piece order, instead of k_seg_reduce after
-    the kernel (PR_SEG_FOLD=0, the default).  Same sums in the same order: bitwise equal
-    ranks, within the oracle bar (Sparky.java:229)."""
-    monkeypatch.setenv("PR_CLASSES", classes)
-    monkeypatch.setenv("PR_HOT_SLOTS", "300")
-    rng = np.random.default_rng(53)
-    V = 60000
-    src, dst = random_edges(rng, V, 400000, hub_frac=0.0)
-    # hubs whose in-links per class exceed one wave unit (512 entries): several pieces each
-    hubs = np.repeat(np.arange(12, dtype=np.int32), 60000)
-    hsrc = rng.integers(0, V, hubs.size).astype(np.int32)
-    src, dst = np.concatenate([src, hsrc]), np.concatenate([dst, hubs])
-    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 6)
-    out = {}
-    for fold in ("1", "0"):
-        monkeypatch.setenv("PR_SEG_FOLD", fold)
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
-            info = g.info()
-            assert info["classes"] == int(classes) and info["n_long_rows"] > 0
-            out[fold], _ = g.run(6)
-            g.reset()
-            g.step(3)  # a second run on the same graph: the arrival counters carry over
-            out[fold + "b"], _ = g.run(6)
-    assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["1b"], out["1"])
-    assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
