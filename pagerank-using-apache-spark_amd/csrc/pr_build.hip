@@ -766,7 +766,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->cbuf[k].alloc(sizeof(double) * (size_t)g->gsize));
     PR_HIP(hipMemsetAsync(g->cbuf[k].p, 0, sizeof(double) * (size_t)g->gsize, s));
   }
-  // k_finalize: one wave per long row, at least 16 workgroups (4096 threads for the <= 2048 block
+  // k_finalize: one wave per long row, at least 16 workgroups (4096 threads for the block
   // partials), at most 512
   g->fin_blocks = (int)std::min<int64_t>(512, std::max<int64_t>(16, (g->n_long + kThreads / kWave - 1) / (kThreads / kWave)));
   PR_TRY(g->fin_part.alloc(sizeof(double) * 2 * g->fin_blocks));
@@ -774,8 +774,11 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
   if (C > 1 && g->epi_grp) {
-    int cap = 2048;
-    if (const char *e = getenv("PR_EPI_BLOCKS")) cap = std::max(atoi(e), 1);  // A/B knob (DESIGN.md §8)
+    // one wave per group, no grid cap: the whole grid in one dispatch lets the workgroups of the
+    // last round finish together (R-MAT s26: 16 K workgroups, -1.8 % per step against a 2048 cap
+    // whose waves stride over 8 groups; profiles/r02/experiments.md)
+    int cap = 1 << 20;
+    if (const char *e = getenv("PR_EPI_BLOCKS")) cap = std::max(atoi(e), 1);  // A/B knob (DESIGN.md §9)
     g->ep_blocks = (int)grid_for((g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G,
                                  kEpiThreads / kWave, cap);
   }

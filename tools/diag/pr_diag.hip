@@ -231,7 +231,7 @@ int prd_time_epi(pr_graph *g, int variant, int iters, double *ms_out) {
   const size_t lds = epi_grp_lds(variant);
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   const int G = kEpiVariants[variant].G;
-  const int blocks = (int)grid_for((g->nblk + G - 1) / G, kEpiThreads / kWave, 2048);
+  const int blocks = (int)grid_for((g->nblk + G - 1) / G, kEpiThreads / kWave, 1 << 20);
   DevBuf part;
   PR_TRY(part.alloc(sizeof(double2) * (size_t)blocks));
   const int in = g->cur, out = g->cur ^ 1;
