@@ -106,7 +106,10 @@ constexpr int64_t kSplitMinSliceBytes = 4ll << 20;
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
 constexpr int kEpiWin = 1024;         // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
-constexpr int kEpiThreads = 256;      // 4 waves, 32.1 KiB of LDS: four workgroups per CU
+#ifndef PR_EPI_THREADS
+#define PR_EPI_THREADS 256  // other values: A/B builds only (-DPR_EPI_THREADS=...)
+#endif
+constexpr int kEpiThreads = PR_EPI_THREADS;  // 4 waves, 32.1 KiB of LDS: four workgroups per CU
 // (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
 struct EpiVariant {
   int G, W;
