@@ -779,8 +779,12 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     // whose waves stride over 8 groups; profiles/r02/experiments.md)
     int cap = 1 << 20;
     if (const char *e = getenv("PR_EPI_BLOCKS")) cap = std::max(atoi(e), 1);  // A/B knob
-    g->ep_blocks = (int)grid_for((g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G,
-                                 kEpiThreads / kWave, cap);
+    // one-wave workgroups pay off when many groups walk (a cheap group's wave frees its LDS
+    // window at once: R-MAT s26 -0.8 %), four-wave ones on uniform graphs (ER s24 +1.3 % narrow)
+    const int64_t ngrp = (g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G;
+    g->epi_narrow = epi_narrow_ok(g->epi_var) && g->n_walk_groups * 10 >= ngrp;
+    if (const char *e = getenv("PR_EPI_NARROW")) g->epi_narrow = epi_narrow_ok(g->epi_var) && atoi(e) != 0;  // A/B
+    g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_var, g->epi_narrow) / kWave, cap);
   }
   else
     g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;

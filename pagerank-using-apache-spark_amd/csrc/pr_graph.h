@@ -77,6 +77,7 @@ struct pr_graph {
   // per-row walk in k_epilogue_grp (PR_EPI_WALK): per group the first of its u16 slot positions
   // in epos, or -1 for the class loop (eoff, i64)
   bool epi_walk = false;
+  bool epi_narrow = false;  // one-wave epilogue workgroups (PR_EPI_NARROW; default: many walking groups)
   int64_t n_walk_groups = 0;
   pr::DevBuf eoff, epos;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;

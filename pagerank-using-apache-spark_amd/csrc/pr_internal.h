@@ -110,11 +110,16 @@ constexpr int kEpiWin = 1024;         // 8 KiB per wave; >= 64 * kEpiGroup + 2 (
 #define PR_EPI_THREADS 256  // other values: A/B builds only (-DPR_EPI_THREADS=...)
 #endif
 constexpr int kEpiThreads = PR_EPI_THREADS;  // 4 waves, 32.1 KiB of LDS: four workgroups per CU
+// narrow grouped epilogue: one-wave workgroups (8.2 KiB of LDS each), so a wave that finishes a
+// cheap group frees its window at once -- chosen when a graph has many walking (sparse) groups
+constexpr int kEpiThreadsNarrow = 64;  // one wave64
 // (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
 struct EpiVariant {
   int G, W;
   bool legacy = false;  // round-1 staging loop (per-class fill accounting) instead of the prefix batches
 };
+inline bool epi_narrow_ok(int var) { return var == 0; }  // one-wave workgroups: variant 0 only
+inline int epi_grp_threads(int var, bool narrow) { return narrow && epi_narrow_ok(var) ? kEpiThreadsNarrow : kEpiThreads; }
 constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016},
                                        {kEpiGroup, kEpiWin, true}, {8, 1272}};
 constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);

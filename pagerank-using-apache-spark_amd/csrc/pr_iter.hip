@@ -155,8 +155,9 @@ int prepare_hot_kernel() {
   for (int v = 0; v < kNumEpiVariants; ++v)
     for (int c : {8, 16, 32, 64, 128})
       for (bool walk : {false, true})
-        PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v, walk)),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v)));
+        for (bool narrow : {false, true})
+          PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v, walk, narrow)),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v, narrow)));
   for (const void *k : {reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, true>),
                         reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1, true>),
                         reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, false>),
@@ -335,9 +336,9 @@ int iter_compute(pr_graph *g) {
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
     if (g->epi_grp) {
-      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var, g->epi_walk);
-      const size_t lds = epi_grp_lds(g->epi_var);
-      hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(kEpiThreads), lds, s, g->nblk, g->partial.as<double>(),
+      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var, g->epi_walk, g->epi_narrow);
+      const size_t lds = epi_grp_lds(g->epi_var, g->epi_narrow);
+      hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_var, g->epi_narrow)), lds, s, g->nblk, g->partial.as<double>(),
                          g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                          g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                          (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,

@@ -927,14 +927,15 @@ __device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
 
 // EDIAG (diagnostics library only; results wrong when != 0): 1 = no partial-run DMA (the window
 // is read as it is), 2 = DMA but no per-class adds, 3 = neither (row data, masks, writes only).
-template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false, int EDIAG = 0>
-__global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
+template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false, int EDIAG = 0,
+          int NT = kEpiThreads>
+__global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part, const int64_t *__restrict__ eoff,
     const uint16_t *__restrict__ epos) {
-  constexpr int NW = kEpiThreads / kWave;
+  constexpr int NW = NT / kWave;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
   static_assert(MW == 1 || MW == 2 || MW == 4, "mask words");
   static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
@@ -1112,7 +1113,7 @@ __global__ __launch_bounds__(kEpiThreads, 4) void k_epilogue_grp(
     }
   }
   double2 *red2 = reinterpret_cast<double2 *>(epi_lds + NW * (W + 2));
-  const double2 part = block_sum2<kEpiThreads>(make_double2(dcp, l1p), red2);
+  const double2 part = block_sum2<NT>(make_double2(dcp, l1p), red2);
   if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
 }
 
@@ -1220,7 +1221,12 @@ using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *
                           const uint16_t *);
 inline bool epi_walk_variant(int C, int var) { return C <= kWave && (var == 0 || var == 7); }
 template <int C>
-inline EpiGrpFn epi_grp_kernel_c(int var, bool walk) {
+inline EpiGrpFn epi_grp_kernel_c(int var, bool walk, bool narrow) {
+  if (narrow && var == 0) {  // one-wave workgroups (variant 0 only)
+    if constexpr (C <= kWave)
+      if (walk) return k_epilogue_grp<C, kEpiGroup, kEpiWin, false, true, 0, kEpiThreadsNarrow>;
+    return k_epilogue_grp<C, kEpiGroup, kEpiWin, false, false, 0, kEpiThreadsNarrow>;
+  }
   if constexpr (C <= kWave) {
     if (walk && var == 7) return k_epilogue_grp<C, kEpiVariants[7].G, kEpiVariants[7].W, false, true>;
     if (walk && var == 0) return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W, false, true>;
@@ -1236,12 +1242,14 @@ inline EpiGrpFn epi_grp_kernel_c(int var, bool walk) {
     default: return k_epilogue_grp<C, kEpiVariants[0].G, kEpiVariants[0].W>;
   }
 }
-inline EpiGrpFn epi_grp_kernel(int C, int var, bool walk = false) {
-  if (C == 128) return epi_grp_kernel_c<128>(var, false);
-  return C == 64 ? epi_grp_kernel_c<64>(var, walk)
-                 : (C == 32 ? epi_grp_kernel_c<32>(var, walk)
-                            : (C == 16 ? epi_grp_kernel_c<16>(var, walk) : epi_grp_kernel_c<8>(var, walk)));
+inline EpiGrpFn epi_grp_kernel(int C, int var, bool walk = false, bool narrow = false) {
+  if (C == 128) return epi_grp_kernel_c<128>(var, false, false);
+  return C == 64 ? epi_grp_kernel_c<64>(var, walk, narrow)
+                 : (C == 32 ? epi_grp_kernel_c<32>(var, walk, narrow)
+                            : (C == 16 ? epi_grp_kernel_c<16>(var, walk, narrow) : epi_grp_kernel_c<8>(var, walk, narrow)));
 }
-inline size_t epi_grp_lds(int var) { return sizeof(double) * (size_t)(kEpiThreads / kWave) * (kEpiVariants[var].W + 4); }
+inline size_t epi_grp_lds(int var, bool narrow = false) {
+  return sizeof(double) * (size_t)(epi_grp_threads(var, narrow) / kWave) * (kEpiVariants[var].W + 4);
+}
 
 }  // namespace pr

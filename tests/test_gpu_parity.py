@@ -555,6 +555,7 @@ def test_epilogue_staging_modes_bitwise(hip, oracle_c, monkeypatch):
     positions, so the row sums -- and the ranks -- are bitwise equal."""
     monkeypatch.setenv("PR_CLASSES", "64")
     monkeypatch.setenv("PR_HOT_SLOTS", "400")
+    monkeypatch.setenv("PR_EPI_NARROW", "0")  # variant 6 has four-wave workgroups only
     rng = np.random.default_rng(31)
     V = 70000
     src, dst = random_edges(rng, V, 900000, hub_frac=0.03)
@@ -579,6 +580,7 @@ def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
     monkeypatch.setenv("PR_CLASSES", classes)
     monkeypatch.setenv("PR_HOT_SLOTS", "400")
     monkeypatch.setenv("PR_EPI_VAR", var)
+    monkeypatch.setenv("PR_EPI_NARROW", "0")  # the same workgroup shape (block partial tree) in every run
     rng = np.random.default_rng(47)
     C = int(classes)
     V = max(90000, 1024 * C)
@@ -605,3 +607,25 @@ def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
             out[walk], _ = g.run(6)
     assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
+
+
+def test_epilogue_narrow_workgroups(hip, oracle_c, monkeypatch):
+    """One-wave epilogue workgroups (PR_EPI_NARROW=1; picked by default when many groups walk)
+    against four-wave ones: the same row sums, the {dangling, L1} block partials in another fixed
+    tree, so the ranks agree to rounding, repeat bitwise, and meet the oracle bar."""
+    monkeypatch.setenv("PR_CLASSES", "32")
+    rng = np.random.default_rng(71)
+    V = 80000
+    src, dst = random_edges(rng, V, 160000, hub_frac=0.02)
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
+    out = {}
+    for narrow in ("1", "0"):
+        monkeypatch.setenv("PR_EPI_NARROW", narrow)
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+            assert g.info()["epilogue"] == 3 and g.info()["walk_groups"] > 0
+            out[narrow], _ = g.run(8)
+            again, _ = g.run(8)
+            assert np.array_equal(again, out[narrow])
+    assert max_rel(out["1"], out["0"]) <= 1e-13
+    assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
+
