@@ -905,7 +905,11 @@ __device__ __forceinline__ int epi_class_add(const uint32_t (&mw)[G], uint32_t b
 // order -- as many steps per batch and block as its busiest row has classes there, instead of
 // one per class -- and the sums are bitwise those of the class loop (whose absent classes add an
 // exact +0).  k_epi_walk_plan plans the positions with the same staging and batching rules.
-// (4 waves per SIMD: the LDS of four workgroups per CU; the register budget keeps the walk there)
+// (at least 4 waves per SIMD: the LDS of four four-wave workgroups per CU; the register budget
+// keeps the walk there.  PR_EPI_MINWAVES: A/B builds only)
+#ifndef PR_EPI_MINWAVES
+#define PR_EPI_MINWAVES 4
+#endif
 // The walk's batches (k_epilogue_grp WALK, k_epi_walk_plan): from class x0, the longest run of
 // classes whose staged runs plus their slots' u16 positions (in 16-byte lanes) fit the window.
 // Lane y holds class y's run prefix (incl, pre) and slot-count prefix (sincl, spre).  One class
@@ -929,7 +933,7 @@ __device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
 // is read as it is), 2 = DMA but no per-class adds, 3 = neither (row data, masks, writes only).
 template <int C, int G = kEpiGroup, int W = kEpiWin, bool LEGACY = false, bool WALK = false, int EDIAG = 0,
           int NT = kEpiThreads>
-__global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
+__global__ __launch_bounds__(NT, PR_EPI_MINWAVES) void k_epilogue_grp(
     int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
