@@ -247,7 +247,7 @@ def _parse_json(text: str):
     JsonReader rules (version unpinned): lenient inputs are parity-unpinned.
     Objects: ("obj", [(key, value), ...]); numbers: _Num (source text)."""
     n = len(text)
-    pos = [5 if text.startswith(")]}'\n") else 0]
+    pos = [0]
 
     def fail(msg):
         raise ValueError(f"JSON: {msg} at {pos[0]}")
@@ -385,6 +385,11 @@ def _parse_json(text: str):
             return None
         return _Num(lit) if _NUMBER.match(lit) else lit
 
+    # consumeNonExecutePrefix: leading whitespace (and, lenient, comments) is skipped first,
+    # then a ")]}'\n" prefix is dropped
+    ws()
+    if text.startswith(")]}'\n", pos[0]):
+        pos[0] += 5
     v = value(0)
     ws()
     if pos[0] != n:

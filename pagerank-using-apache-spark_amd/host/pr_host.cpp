@@ -116,7 +116,9 @@ class JParser {
  public:
   JParser(const char *p, const char *e) : p_(p), e_(e) {}
   bool parse(JVal &out) {
+    // Gson's consumeNonExecutePrefix skips leading whitespace (and, lenient, comments) first
     static const char kPrefix[] = ")]}'\n";
+    if (!ws()) return false;
     if ((size_t)(e_ - p_) >= 5 && std::memcmp(p_, kPrefix, 5) == 0) p_ += 5;
     if (!value(out, 0)) return false;
     if (!ws()) return false;

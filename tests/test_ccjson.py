@@ -148,3 +148,14 @@ def test_ccjson_lenient_still_rejects(bad):
         native(f"http://bad.com/\t{bad}\n")
     with pytest.raises(ValueError):
         sparky_rdd.pairs_from_ccjson_lines([f"http://bad.com/\t{bad}"])
+
+
+def test_nonexecute_prefix_after_leading_whitespace():
+    """Gson's consumeNonExecutePrefix skips leading whitespace and (lenient) comments before it
+    looks for ")]}'\\n" (ADVICE r2); the native parser (pr_host.cpp JParser::parse) applies the same
+    rule.  A line-framed record cannot hold the prefix's newline, so this is checked on the
+    restatement's parser directly."""
+    for text in (")]}'\n{\"a\": 1}", "  )]}'\n{\"a\": 1}", "\t/* c */ )]}'\n {\"a\": 1}"):
+        assert sparky_rdd._parse_json(text) == ("obj", [("a", sparky_rdd._Num("1"))])
+    with pytest.raises(ValueError):
+        sparky_rdd._parse_json("x )]}'\n{\"a\": 1}")

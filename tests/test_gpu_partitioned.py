@@ -1,0 +1,122 @@
+"""The row-partitioned path at the BASELINE.json sizes that name P > 1, against
+the oracle on an independently built CSR.
+
+BASELINE.json configs[2] (Erdos-Renyi s24 at 2/4/8 GPUs), configs[3] (R-MAT s26 at 2/4/8) and
+configs[4] (the Twitter shape at 8) run 1D row-partitioned with one exchange per iteration -- the
+replacement of Sparky.java:192's per-iteration join re-shuffle.  This pool has one GPU per box and
+RCCL refuses two ranks on one device (tools/rccl_probe.py), so the P parts run as a single-process
+group on one GPU (pr_group_*): every part is built by the product path with the default policy
+(classes from the part's expected gather space, sparse exchange into a compacted gather space),
+and the parts exchange exactly the runs RCCL's send/recv would carry, by device copies.
+
+Per config, against oracle/pagerank_oracle.c (the restatement of Sparky.java:98-235) on the CSR
+it builds itself from the raw interned edges:
+* every vertex is owned by exactly one part, and the parts' in-links add up to E';
+* ranks after each of 10 iterations (Sparky.java:187): max relative error <= 1e-9;
+* dc (Sparky.java:219-222) and the L1 delta of every iteration: relative 1e-9;
+* the overlapped exchange (pr_set_option PR_OPT_XCHG_CHUNKS: one chunk per hot phase) gives the
+  same ranks bit for bit as whole runs, so both exchange modes meet the same bar.
+"""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RANK_TOL = 1e-9  # north_star: "ranks within 1e-9 max relative error"
+ITERS = 10  # Sparky.java:187
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import sparky_hip
+
+    assert sparky_hip.device_count() > 0, "no GPU visible: the gpu tests need an MI355X"
+    return sparky_hip
+
+
+def max_rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b) / np.abs(b))) if a.size else 0.0
+
+
+def group_iterations(hip, grp, parts, V, iters):
+    """Per iteration: the merged ranks (each part writes only its own vertices) and part 0's view
+    of dc / L1 (every part sums all parts' slots in part order, so any part reports the same)."""
+    grp.reset()
+    hist, dcs, l1s = [], [], []
+    for _ in range(iters):
+        grp.step(1)
+        grp.sync()
+        hist.append(grp.ranks())
+        st = parts[0].stats()
+        dcs.append(st["last_dc"])
+        l1s.append(st["last_l1"])
+    return hist, dcs, l1s
+
+
+@pytest.mark.parametrize("graph,scale,P", [("rmat", 26, 8), ("rmat", 26, 2), ("er", 24, 4), ("twitter", 0, 8)],
+                         ids=["rmat-s26-P8", "rmat-s26-P2", "er-s24-P4", "twitter-P8"])
+def test_partitioned_config_parity(hip, oracle_c, graph, scale, P):
+    import torch
+
+    from sparky_hip.workloads import generate
+
+    t0 = time.perf_counter()
+    wl = generate(graph, scale=scale)
+    torch.cuda.synchronize()
+    V, E = wl.n_vertices, wl.n_edges
+    parts = []
+    try:
+        for p in range(P):
+            parts.append(hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device_input=True, n_edges=E,
+                                           part=p, n_parts=P, keep_canonical=False))
+        hs, hd = wl.src.cpu().numpy(), wl.dst.cpu().numpy()
+        del wl
+        torch.cuda.empty_cache()
+        infos = [p.info() for p in parts]
+        t_build = time.perf_counter()
+        csr = oracle_c.build_csr(V, hs, hd)
+        del hs, hd
+        t_orc = time.perf_counter()
+
+        # the partition: every vertex owned once, every in-link owned once
+        assert sum(i["local_rows"] for i in infos) == V
+        assert sum(i["local_edges"] for i in infos) == csr.n_edges
+        assert all(i["n_edges"] == csr.n_edges and i["n_parts"] == P for i in infos)
+        assert sum(i["xchg_send"] for i in infos) == sum(i["xchg_recv"] for i in infos)
+        grp = hip.PartGroup(parts)
+        grp.reset()
+        owners = np.zeros(V, np.int32)
+        for p in parts:
+            probe = np.full(V, np.nan)
+            p.ranks(probe)
+            owners += ~np.isnan(probe)
+        assert owners.min() == 1 and owners.max() == 1, "a vertex is owned by no part or by two"
+
+        hist, dcs, l1s = group_iterations(hip, grp, parts, V, ITERS)
+        for p in parts:
+            p.set_exchange_chunks(True)
+        hist_c, dcs_c, l1s_c = group_iterations(hip, grp, parts, V, ITERS)
+        chunked = [p.info()["classes"] >= 16 for p in parts]
+        for p in parts:
+            p.set_exchange_chunks(False)
+    finally:
+        for p in parts:
+            p.close()
+    t_gpu = time.perf_counter()
+    ref = oracle_c.run(csr, ITERS, keep_history=True)
+    t_ref = time.perf_counter()
+    errs = [max_rel(hist[it], ref["history"][it]) for it in range(ITERS)]
+    print(f"\n{graph} s{scale} P={P}: V={V} E'={csr.n_edges} classes={[i['classes'] for i in infos]} "
+          f"recv/part={[i['xchg_recv'] for i in infos]} chunked={chunked} "
+          f"max_rel per iteration {['%.1e' % e for e in errs]}; gen+build {t_build - t0:.1f}s "
+          f"oracle build {t_orc - t_build:.1f}s gpu {t_gpu - t_orc:.1f}s oracle run {t_ref - t_gpu:.1f}s")
+    for it in range(ITERS):
+        assert errs[it] <= RANK_TOL, (it, errs[it])
+        assert abs(dcs[it] - ref["dc"][it]) <= RANK_TOL * max(abs(ref["dc"][it]), 1.0), it
+        assert abs(l1s[it] - ref["l1"][it]) <= RANK_TOL * max(ref["l1"][it], 1.0), it
+        # the overlapped exchange moves the same values, only earlier: bitwise the same iteration
+        assert np.array_equal(hist_c[it], hist[it]), it
+        assert dcs_c[it] == dcs[it] and l1s_c[it] == l1s[it], it
