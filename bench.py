@@ -18,6 +18,11 @@ Rank 0 prints ONE JSON line (the driver's contract), including
   parity_max_rel: after the timed region, K iterations from a fresh reset on the GPU (every
                   rank's rows summed into one vector on rank 0 when N > 1) against K iterations
                   of the oracle on the exported canonical CSR -- the north-star 1e-9 bar;
+  error (only on failure): a watchdog thread gives every stage (init, generate, build, attach,
+                  calibration, timed, parity) a deadline; a stage that overruns -- e.g. a hang
+                  inside ncclCommInitRank or a collective on a first multi-GPU run -- makes rank 0
+                  print the JSON line with "value": null and "error" naming the stage, and every
+                  rank exit with status 3 (no re-exec; the process ends itself)
   exchange_overlap_ab (N > 1): a calibration before the timed region runs max(5, K/2) steps
                   with the exchange after the pass (the library default) and overlapped with the
                   next iteration's SpMV phases (pr_set_option) with 0/1/2 CUs per XCD kept free for
@@ -31,6 +36,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -44,6 +50,51 @@ LAYOUT_VERSION = "split-c64-phased-grpepi2-nt-mik-ldsassign-order1-b128-walk-epi
 
 def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+STAGES = ("init", "generate", "build", "attach", "calibration", "timed", "parity")
+
+
+class Watchdog:
+    """Per-stage deadlines in a daemon thread of this process.  On expiry rank 0 prints the
+    contract's JSON line with "value": null and an "error" naming the stage, then every rank ends
+    with os._exit(3): a hang in RCCL (ncclCommInitRank, a grouped send/recv) or anywhere else can
+    never leave the driver without a line.  The thread only reads the clock; it touches no GPU."""
+
+    def __init__(self, rank: int, world: int, steps: int, warmup: int):
+        self.rank, self.world, self.steps, self.warmup = rank, world, steps, warmup
+        self._lock = threading.Lock()
+        self._stage, self._limit, self._t0 = None, None, 0.0
+        threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def enter(self, stage: str, seconds: float) -> None:
+        with self._lock:
+            self._stage, self._limit, self._t0 = stage, float(seconds), time.monotonic()
+
+    def done(self) -> None:
+        with self._lock:
+            self._stage = None
+
+    def error_line(self, stage: str, limit: float) -> dict:
+        return {"metric": METRIC, "value": None, "unit": "GTEPS", "n_gpus": self.world, "steps": self.steps,
+                "warmup": self.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+                "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded device-side generator; no dataset)",
+                "config": {"workload": None}, "roofline": None, "cpu_baseline": None,
+                "error": f"stage '{stage}' exceeded its {limit:.0f} s deadline on rank {self.rank} (hang?)"}
+
+    def _watch(self) -> None:
+        while True:
+            time.sleep(0.2)
+            with self._lock:
+                stage, limit, t0 = self._stage, self._limit, self._t0
+            if stage is None or time.monotonic() - t0 <= limit:
+                continue
+            line = self.error_line(stage, limit)
+            log(line["error"])
+            if self.rank == 0:
+                print(json.dumps(line), flush=True)
+            sys.stderr.flush()
+            os._exit(3)
 
 
 def pmc_traffic(workload: str):
@@ -128,7 +179,23 @@ def main() -> int:
     ap.add_argument("--parity-iters", type=int, default=10, help="K of the parity / cpu_baseline leg (Sparky.java:187)")
     ap.add_argument("--no-overlap-ab", action="store_true",
                     help="N > 1: skip the exchange-mode calibration and time the library default")
+    ap.add_argument("--stage-timeout", type=float, default=None,
+                    help="deadline of every stage in seconds (default: per stage, 180-900 s)")
+    ap.add_argument("--simulate-stall", choices=STAGES, default=None,
+                    help="test hook: hang in this stage (before any GPU work) to exercise the watchdog")
     a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    limits = {"init": 300, "generate": 300, "build": 600, "attach": 180, "calibration": 600, "timed": 600, "parity": 900}
+    if a.stage_timeout is not None:
+        limits = {k: a.stage_timeout for k in limits}
+    wd = Watchdog(rank, world, a.steps, a.warmup)
+    if a.simulate_stall:
+        wd.enter(a.simulate_stall, limits[a.simulate_stall])
+        while True:
+            time.sleep(1.0)
 
     import numpy as np
     import torch
@@ -136,12 +203,10 @@ def main() -> int:
     import sparky_hip
     from sparky_hip.workloads import generate
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
     dev = local_rank
+    wd.enter("init", limits["init"])
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
@@ -150,12 +215,14 @@ def main() -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
 
+    wd.enter("generate", limits["generate"])
     t0 = time.perf_counter()
     wl = generate(a.graph, scale=a.scale, edge_factor=a.edge_factor, seed=a.seed, device=dev)
     V, E, workload = wl.n_vertices, wl.n_edges, wl.description
     t_gen = time.perf_counter() - t0
     log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
     validate = not a.no_cpu_baseline
+    wd.enter("build", limits["build"])
     g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
                                  n_edges=E, part=rank, n_parts=world, keep_canonical=(validate and rank == 0),
                                  layout=a.layout)
@@ -164,6 +231,7 @@ def main() -> int:
     info = g.info()
     log(f"rank {rank}: build {g.stats()['build_ms']:.0f} ms; info {info}")
     if world > 1:
+        wd.enter("attach", limits["attach"])
         obj = [sparky_hip.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         g.attach_comm(rank, world, obj[0])
@@ -195,6 +263,7 @@ def main() -> int:
             dist.all_reduce(tc, op=dist.ReduceOp.MAX)
             return round(float(tc.item()) / max(k, 1) * 1e3, 4)
 
+        wd.enter("calibration", limits["calibration"])
         k_cal = max(5, a.steps // 2)
         overlap = {"calibration_steps": k_cal, "chunks": info.get("classes", 1) // 8, "library_default": "unchunked"}
         best = None
@@ -212,6 +281,7 @@ def main() -> int:
         overlap["chosen"] = mode[0]
         log(f"exchange mode calibration: {overlap}")
 
+    wd.enter("timed", limits["timed"])
     g.reset()
     g.step(a.warmup)
     g.sync()
@@ -251,6 +321,7 @@ def main() -> int:
 
     # ---- validation leg (after the timed region): K iterations from a fresh reset vs the oracle ----
     cpu, parity = None, None
+    wd.enter("parity", limits["parity"])
     if validate:
         K = a.parity_iters
 
@@ -310,6 +381,7 @@ def main() -> int:
         if dist is not None:
             dist.barrier()
     g.close()
+    wd.done()
 
     if rank == 0:
         line = {
