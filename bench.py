@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 METRIC = "PageRank GTEPS/iter + % HBM roofline, R-MAT scale-26 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 # bumped whenever the SpMV pass changes, so a stale rocprof traffic figure is never reported
-LAYOUT_VERSION = "split-c64-phased-grpepi2-nt-mik-ldsassign-order1-b128-walk-epigrid-narrow-v9"
+LAYOUT_VERSION = "r3-split-c64-grpepi-walk-narrow+rows-t1024-r17-v10"
 
 
 def log(msg: str) -> None:
@@ -98,15 +98,21 @@ class Watchdog:
 
 
 def pmc_traffic(workload: str):
-    """Per-pass HBM bytes of the SpMV kernels from a committed rocprofv3 PMC summary."""
+    """HBM bytes per launch of the pass's dominant kernel and per pass, from the committed
+    rocprofv3 PMC summary of this workload (profiles/pmc_spmv.json, tools/pmc_summary.py), or
+    None when none matches this build's LAYOUT_VERSION."""
     path = os.path.join(ROOT, "profiles", "pmc_spmv.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload and d.get("layout_version") == LAYOUT_VERSION:
-            return d.get("hbm_bytes_per_pass")
+        if d.get("layout_version") != LAYOUT_VERSION:
+            return None
+        rec = d.get("workloads", {}).get(workload)
+        if rec:
+            return {"kernel": rec.get("kernel"), "per_launch": rec.get("hbm_bytes_per_launch"),
+                    "per_pass": rec.get("hbm_bytes_per_pass"), "l2_hit_rate": rec.get("l2_hit_rate")}
     except Exception:
         return None
     return None
@@ -173,12 +179,15 @@ def main() -> int:
     ap.add_argument("--graph", choices=["rmat", "er", "lj", "twitter"], default="rmat",
                     help="lj / twitter: the Chung-Lu shapes of BASELINE.json configs[1] / [4]")
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--layout", choices=["auto", "fused", "split"], default="auto",
+    ap.add_argument("--layout", choices=["auto", "fused", "split", "rows"], default="auto",
                     help="graph layout (A/B; auto picks by gather-space size)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (no cpu_baseline, no parity)")
     ap.add_argument("--parity-iters", type=int, default=10, help="K of the parity / cpu_baseline leg (Sparky.java:187)")
     ap.add_argument("--no-overlap-ab", action="store_true",
                     help="N > 1: skip the exchange-mode calibration and time the library default")
+    ap.add_argument("--build-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="pr_graph_create_ex build option (A/B), e.g. classes=32, hot_slots=9000, "
+                         "exchange_allgather=1; repeatable")
     ap.add_argument("--stage-timeout", type=float, default=None,
                     help="deadline of every stage in seconds (default: per stage, 180-900 s)")
     ap.add_argument("--simulate-stall", choices=STAGES, default=None,
@@ -223,9 +232,10 @@ def main() -> int:
     log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
     validate = not a.no_cpu_baseline
     wd.enter("build", limits["build"])
+    bopts = {k: int(v) for k, v in (o.split("=", 1) for o in a.build_option)}
     g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
                                  n_edges=E, part=rank, n_parts=world, keep_canonical=(validate and rank == 0),
-                                 layout=a.layout)
+                                 layout=a.layout, options=bopts)
     del wl
     torch.cuda.empty_cache()
     info = g.info()
@@ -236,7 +246,7 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         g.attach_comm(rank, world, obj[0])
 
-    xchg_desc = (" + RCCL all-gather of whole slices" if os.environ.get("PR_EXCHANGE") == "allgather"
+    xchg_desc = (" + RCCL all-gather of whole slices" if bopts.get("exchange_allgather")
                  else " + RCCL grouped send/recv of the needed contributions")
 
     # N > 1: the exchange mode of the timed run is calibrated first -- whole runs after the pass
@@ -406,6 +416,9 @@ def main() -> int:
                 "exchange_mode": mode[0] if world > 1 else None,
                 "exchange_doubles_per_iter_rank0": info.get("xchg_send", 0) if world > 1 else 0,
                 "iterations_timed": a.steps,
+                "build_options": bopts or None,
+                "layout": ["fused", "split", "rows"][info.get("layout", 0)],
+                "hot_cover": round(info.get("hot_cover_ppm", 0) / 1e6, 4),
             },
             "roofline": {
                 "bound": "hbm",
@@ -414,12 +427,14 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(workload) if world == 1 else None,
-                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue[_grp] (split layout, {info.get('classes')} "
-                           "column classes, run per XCD in phases)" if info.get("classes", 1) > 1
-                           else "spmv pass: k_spmv_units (fused layout)"),
+                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue_grp (split layout, {info.get('classes')} "
+                           "column classes, run per XCD in phases)" if info.get("layout") == 1
+                           else ("spmv pass: k_spmv_rows (row-block layout, LDS row sums, update fused)"
+                                 if info.get("layout") == 2 else "spmv pass: k_spmv_units (fused layout)")),
                 "classes": info.get("classes"),
                 "bytes_model": "12*E'_part + 36*V_part per launch (pull-fp64-v1)",
                 "spmv_ms_mean": round(spmv_ms, 4),
+                "launches_per_pass": info.get("launches", 1),
                 "iter_ms_mean_events": round(st["iter_ms_mean"], 4),
                 "exchange_ms_mean": round(st["exchange_ms_mean"], 4),
             },

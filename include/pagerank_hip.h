@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PR_ABI_VERSION 1
+#define PR_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------------------- */
 #define PR_OK 0
@@ -44,6 +44,7 @@ extern "C" {
 #define PR_NO_CANONICAL 4u   /* drop the canonical CSR after the build (no export)        */
 #define PR_LAYOUT_FUSED 8u   /* force the single-pass layout (default: chosen by size)    */
 #define PR_LAYOUT_SPLIT 16u  /* force the per-XCD column-class layout                     */
+#define PR_LAYOUT_ROWS 32u   /* force the row-block layout (LDS row sums, no partial slots)  */
 
 /* ---- vertex flag bits (pr_graph_export_csr vflags) ---------------------------------- */
 #define PR_VF_KEY 1u    /* vertex is a record key / src          Sparky.java:127-135      */
@@ -70,10 +71,13 @@ extern "C" {
 #define PR_INFO_XCHG_RECV 15   /* doubles this part receives per iteration (P > 1)        */
 #define PR_INFO_PARTIAL_SLOTS 16 /* (row, column class) segment sums of the split layout     */
 #define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
-#define PR_INFO_EPILOGUE 18    /* 0 fused, 1 per-block, 2 per-class buffers, 3 grouped      */
+#define PR_INFO_EPILOGUE 18    /* 0 fused units, 3 grouped (split), 4 fused into row tiles   */
 #define PR_INFO_GATHER_EST 19  /* bytes of the part's expected gather space (class policy)   */
 #define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
-#define PR_INFO_COUNT 21
+#define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots), 2 rows  */
+#define PR_INFO_HOT_COVER 22   /* in-links read from the LDS hot sets, parts per million      */
+#define PR_INFO_LAUNCHES 23    /* launches of the dominant SpMV kernel per iteration (row-block passes) */
+#define PR_INFO_COUNT 24
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */
@@ -81,7 +85,8 @@ extern "C" {
 #define PR_STAT_LAST_L1 2        /* sum |r_k - r_{k-1}| of the last iteration                */
 #define PR_STAT_SPMV_MS_MEAN 3   /* mean HIP-event time of the SpMV launch (timing on)      */
 #define PR_STAT_SPMV_LAUNCHES 4  /* SpMV launches timed                                     */
-#define PR_STAT_ITER_MS_MEAN 5   /* mean HIP-event time of a whole iteration (timing on)    */
+#define PR_STAT_ITER_MS_MEAN 5   /* mean HIP-event time of a whole iteration, its exchange
+                                    included (timing on)                                    */
 #define PR_STAT_BUILD_MS 6       /* wall time of the graph build                            */
 #define PR_STAT_EXCHANGE_MS_MEAN 7 /* mean time of the RCCL exchange (parts > 1)            */
 #define PR_STAT_COUNT 8
@@ -114,6 +119,21 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
                          int64_t n_edges, const int32_t *src, const int32_t *dst, uint32_t flags,
                          pr_graph **out);
 
+/* The same with build options: n_options (key, value) pairs of int64 in `options` (may be NULL
+ * when n_options is 0).  They tune the layout (A/B, tests); results do not depend on them beyond
+ * summation order.  An unknown key or an out-of-range value fails with PR_ERR_INVALID.  The library
+ * reads no environment variables: every choice is an explicit option. */
+#define PR_BOPT_CLASSES 1     /* column classes of the split layout: 0 (size policy), 8, 16, 32, 64, 128 */
+#define PR_BOPT_HOT_SLOTS 2   /* LDS hot-set slots per class: -1 (default 18430) or 0..18430            */
+#define PR_BOPT_EXCHANGE 3    /* P > 1: 0 per-peer runs (default), 1 whole-slice all-gather (all parts alike) */
+#define PR_BOPT_XCHG_CHUNKS 4 /* P > 1: 1 = the overlapped exchange from the start (PR_OPT_XCHG_CHUNKS) */
+#define PR_BOPT_HOT_RESERVE 5 /* CUs per XCD the heavy SpMV kernel leaves free, 0..3 (PR_OPT_HOT_RESERVE) */
+#define PR_BOPT_EPI_WALK 6    /* split layout: 1 (default) per-row walk of sparse epilogue groups, 0 never */
+#define PR_BOPT_EPI_NARROW 7  /* split layout: -1 auto (default), 0 four-wave, 1 one-wave epilogue workgroups */
+int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
+                       const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
+                       int32_t n_options, pr_graph **out);
+
 /* info[i] for i < min(n_info, PR_INFO_COUNT). */
 int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info);
 
@@ -143,8 +163,8 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 
 /* Execution options (no effect on results; A/B and tuning).  PR_OPT_XCHG_CHUNKS: 1 = the
  * exchange of a part with peers travels in one chunk per SpMV phase and the next iteration's
- * phase c waits only for chunk c (overlap), 0 = whole runs (the default; PR_XCHG_CHUNKS sets it
- * at build).  With RCCL every rank must make the same call (it is collective: the ranks check
+ * phase c waits only for chunk c (overlap), 0 = whole runs (the default; PR_BOPT_XCHG_CHUNKS sets
+ * it at build).  With RCCL every rank must make the same call (it is collective: the ranks check
  * that they agree, so a mismatch fails instead of hanging); in a group, set every part alike. */
 #define PR_OPT_XCHG_CHUNKS 1
 /* PR_OPT_HOT_RESERVE: CUs per XCD that the heavy SpMV kernel leaves free (0..3, default 0), for
@@ -155,7 +175,7 @@ int pr_set_option(pr_graph *g, int32_t option, int64_t value);
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes
  * to every rank (any channel), every rank attaches it to its part.  Once per iteration each
  * part sends every peer exactly the contributions (and the two dangling/L1 slots) that the
- * peer's in-links read, with grouped RCCL ncclSend/ncclRecv over xGMI (PR_EXCHANGE=allgather:
+ * peer's in-links read, with grouped RCCL ncclSend/ncclRecv over xGMI (PR_BOPT_EXCHANGE = 1:
  * one ncclAllGather of whole slices instead).  Attach cross-checks the per-peer run lengths. */
 #define PR_COMM_ID_BYTES 128
 int pr_comm_unique_id(uint8_t *id_out);

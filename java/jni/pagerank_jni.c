@@ -39,6 +39,12 @@ static jdoubleArray fail(JNIEnv *env, int rc) {
   return NULL;
 }
 
+JNIEXPORT jint JNICALL Java_sparky_hip_PageRankJni_abiVersion(JNIEnv *env, jclass cls) {
+  (void)env;
+  (void)cls;
+  return (jint)pr_abi_version();
+}
+
 JNIEXPORT jdoubleArray JNICALL Java_sparky_hip_PageRankJni_run(JNIEnv *env, jclass cls, jint device, jint n_vertices,
                                                                jintArray jsrc, jintArray jdst, jint flags,
                                                                jint iterations, jdoubleArray jinit, jobject listener,
@@ -47,8 +53,15 @@ JNIEXPORT jdoubleArray JNICALL Java_sparky_hip_PageRankJni_run(JNIEnv *env, jcla
   const jsize E = (*env)->GetArrayLength(env, jsrc);
   if ((*env)->GetArrayLength(env, jdst) != E) return fail(env, PR_ERR_INVALID);
   if (jinit && (*env)->GetArrayLength(env, jinit) != n_vertices) return fail(env, PR_ERR_INVALID);
+  /* Get*ArrayElements / malloc return NULL on OOM (an OutOfMemoryError is then pending for the
+   * JNI calls): release what was obtained and return */
   jint *src = (*env)->GetIntArrayElements(env, jsrc, NULL);
+  if (!src) return NULL;
   jint *dst = (*env)->GetIntArrayElements(env, jdst, NULL);
+  if (!dst) {
+    (*env)->ReleaseIntArrayElements(env, jsrc, src, JNI_ABORT);
+    return NULL;
+  }
   pr_graph *g = NULL;
   int rc = pr_graph_create(device, n_vertices, (int64_t)E, (const int32_t *)src, (const int32_t *)dst,
                            (uint32_t)flags | PR_NO_CANONICAL, &g);
@@ -56,8 +69,19 @@ JNIEXPORT jdoubleArray JNICALL Java_sparky_hip_PageRankJni_run(JNIEnv *env, jcla
   (*env)->ReleaseIntArrayElements(env, jdst, dst, JNI_ABORT);
   if (rc != PR_OK) return fail(env, rc);
   double *init = NULL;
-  if (jinit) init = (double *)(*env)->GetDoubleArrayElements(env, jinit, NULL);
+  if (jinit) {
+    init = (double *)(*env)->GetDoubleArrayElements(env, jinit, NULL);
+    if (!init) {
+      pr_graph_destroy(g);
+      return NULL;
+    }
+  }
   double *ranks = (double *)malloc(sizeof(double) * (size_t)(n_vertices > 0 ? n_vertices : 1));
+  if (!ranks) {
+    if (jinit) (*env)->ReleaseDoubleArrayElements(env, jinit, (jdouble *)init, JNI_ABORT);
+    pr_graph_destroy(g);
+    return fail(env, PR_ERR_OOM);
+  }
   cb_ctx ctx = {env, listener, NULL, n_vertices, 0};
   if (listener) {
     jclass lc = (*env)->GetObjectClass(env, listener);

@@ -29,13 +29,9 @@ public final class PageRankHip implements AutoCloseable {
     /** pr_graph_create flags (include/pagerank_hip.h). */
     public static final int PR_DANGLING_LOCAL = 0, PR_DANGLING_NONE = 1, PR_NO_CANONICAL = 4;
     static final int PR_CB_RANKS = 1;
-    static final int PR_INFO_COUNT = 21;
-
-    /** Per-iteration hook: ranks is null unless requested (original-ID order, V doubles). */
-    @FunctionalInterface
-    public interface IterationListener {
-        void onIteration(int iteration, double[] ranks, double danglingSum, double l1Delta, double ms);
-    }
+    static final int PR_INFO_COUNT = 24;
+    /** PR_ABI_VERSION of include/pagerank_hip.h this binding was written against. */
+    public static final int ABI_VERSION = 2;
 
     private static final Linker LINKER = Linker.nativeLinker();
     private static final SymbolLookup LIB = SymbolLookup.libraryLookup(
@@ -54,6 +50,19 @@ public final class PageRankHip implements AutoCloseable {
             ADDRESS, ADDRESS, JAVA_INT));
     private static final MethodHandle DESTROY = h("pr_graph_destroy", FunctionDescriptor.ofVoid(ADDRESS));
     private static final MethodHandle LAST_ERROR = h("pr_last_error", FunctionDescriptor.of(ADDRESS));
+    private static final MethodHandle ABI = h("pr_abi_version", FunctionDescriptor.of(JAVA_INT));
+
+    static {
+        try {
+            int v = (int) ABI.invokeExact();
+            if (v != ABI_VERSION)
+                throw new UnsatisfiedLinkError("libpagerank_hip ABI " + v + ", this binding needs " + ABI_VERSION);
+        } catch (UnsatisfiedLinkError e) {
+            throw e;
+        } catch (Throwable t) {
+            throw new ExceptionInInitializerError(t);
+        }
+    }
     private static final FunctionDescriptor CB_DESC = FunctionDescriptor.ofVoid(
             JAVA_INT, ADDRESS, JAVA_DOUBLE, JAVA_DOUBLE, JAVA_DOUBLE, ADDRESS);
 

@@ -43,9 +43,10 @@ void DevBuf::reset() {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hmeta.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
+  b += tile_u.bytes + rcodes.bytes + rrows.bytes;
   return b;
 }
 
@@ -75,21 +76,66 @@ int check_device(int32_t device) {
   return PR_OK;
 }
 
+// (key, value) build options -> g->opts (PR_BOPT_*); an unknown key or a value out of range fails
+int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
+  if (n < 0 || (n > 0 && !options)) return fail(PR_ERR_INVALID, "options is NULL");
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t k = options[2 * i], v = options[2 * i + 1];
+    switch (k) {
+      case PR_BOPT_CLASSES:
+        if (v != 0 && v != 8 && v != 16 && v != 32 && v != 64 && v != 128)
+          return fail(PR_ERR_INVALID, "PR_BOPT_CLASSES: 0 (policy), 8, 16, 32, 64 or 128");
+        o->classes = (int)v;
+        break;
+      case PR_BOPT_HOT_SLOTS:
+        if (v < -1 || v > pr::kHotSlotsMax) return fail(PR_ERR_INVALID, "PR_BOPT_HOT_SLOTS: -1 (default) or 0..18430");
+        o->hot_slots = (int)v;
+        break;
+      case PR_BOPT_EXCHANGE:
+        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EXCHANGE: 0 (runs) or 1 (all-gather)");
+        o->allgather = v == 1;
+        break;
+      case PR_BOPT_XCHG_CHUNKS:
+        o->xchg_chunks = v != 0;
+        break;
+      case PR_BOPT_HOT_RESERVE:
+        if (v < 0 || v > 3) return fail(PR_ERR_INVALID, "PR_BOPT_HOT_RESERVE: 0..3 CUs per XCD");
+        o->hot_reserve = (int)v;
+        break;
+      case PR_BOPT_EPI_WALK:
+        o->epi_walk = v != 0;
+        break;
+      case PR_BOPT_EPI_NARROW:
+        if (v < -1 || v > 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_NARROW: -1 (auto), 0 or 1");
+        o->epi_narrow = (int)v;
+        break;
+      default:
+        return fail(PR_ERR_INVALID, "unknown build option " + std::to_string(k));
+    }
+  }
+  return PR_OK;
+}
+
 int create_common(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
-                  const int32_t *src, const int32_t *dst, uint32_t flags, pr_graph **out) {
+                  const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
+                  int32_t n_options, pr_graph **out) {
   if (!out) return fail(PR_ERR_INVALID, "out is NULL");
   *out = nullptr;
   if (n_parts < 1 || part < 0 || part >= n_parts) return fail(PR_ERR_INVALID, "bad part / n_parts");
   if (n_parts > pr::kMaxParts) return fail(PR_ERR_INVALID, "n_parts above 64 is not supported");
   if (n_vertices < 0 || n_edges < 0) return fail(PR_ERR_INVALID, "negative size");
   if (n_edges > 0 && (!src || !dst)) return fail(PR_ERR_INVALID, "src/dst is NULL");
-  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT))
+  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT | PR_LAYOUT_ROWS))
     return fail(PR_ERR_INVALID, "unknown flag bits");
-  if ((flags & PR_LAYOUT_FUSED) && (flags & PR_LAYOUT_SPLIT)) return fail(PR_ERR_INVALID, "PR_LAYOUT_FUSED and PR_LAYOUT_SPLIT are exclusive");
+  const uint32_t lay = flags & (PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT | PR_LAYOUT_ROWS);
+  if (lay & (lay - 1)) return fail(PR_ERR_INVALID, "PR_LAYOUT_FUSED / _SPLIT / _ROWS are exclusive");
+  pr_build_opts opts;
+  PR_TRY(parse_options(options, n_options, &opts));
   PR_TRY(check_device(device));
   DeviceGuard dg(device);
   pr_graph *g = new (std::nothrow) pr_graph();
   if (!g) return fail(PR_ERR_OOM, "host allocation failed");
+  g->opts = opts;
   g->device = device;
   g->flags = flags;
   g->V = n_vertices;
@@ -132,16 +178,22 @@ int pr_device_count(int32_t *out) {
 
 int pr_graph_create(int32_t device, int32_t n_vertices, int64_t n_edges, const int32_t *src,
                     const int32_t *dst, uint32_t flags, pr_graph **out) {
-  return create_common(device, 0, 1, n_vertices, n_edges, src, dst, flags, out);
+  return create_common(device, 0, 1, n_vertices, n_edges, src, dst, flags, nullptr, 0, out);
 }
 
 int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices,
                          int64_t n_edges, const int32_t *src, const int32_t *dst, uint32_t flags,
                          pr_graph **out) {
-  return create_common(device, part, n_parts, n_vertices, n_edges, src, dst, flags, out);
+  return create_common(device, part, n_parts, n_vertices, n_edges, src, dst, flags, nullptr, 0, out);
 }
 
-// doubles moved per iteration by this part: the packed runs, or whole slices (PR_EXCHANGE=allgather)
+int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
+                       const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
+                       int32_t n_options, pr_graph **out) {
+  return create_common(device, part, n_parts, n_vertices, n_edges, src, dst, flags, options, n_options, out);
+}
+
+// doubles moved per iteration by this part: the packed runs, or whole slices (PR_BOPT_EXCHANGE = 1)
 static int64_t xchg_volume(const pr_graph *g, bool send) {
   if (g->nparts <= 1) return 0;
   if (g->x_allgather) return (send ? 1 : g->nparts - 1) * g->S_pad;
@@ -153,11 +205,13 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
-                                    g->n_units + g->n_hunits, g->n_long + g->n_segs, (int64_t)g->device_bytes(), g->C,
+                                    g->n_units + g->n_hunits + g->n_runits, g->n_long + g->n_segs,
+                                    (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->C == 1 ? 0 : (g->epi_grp ? 3 : (g->epi_abs ? 1 : 2)), g->gather_est,
-                                    g->n_walk_groups};
+                                    g->layout == pr::kLayoutRows ? 4 : (g->C == 1 ? 0 : 3), g->gather_est,
+                                    g->n_walk_groups, g->layout, g->hot_cover_ppm,
+                                    g->layout == pr::kLayoutRows ? g->rows_passes : 1};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }
@@ -266,7 +320,21 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
   }
   PR_TRY(mean_ms(g->spmv_ev, &v[PR_STAT_SPMV_MS_MEAN]));
   v[PR_STAT_SPMV_LAUNCHES] = (double)g->spmv_ev.size();
-  PR_TRY(mean_ms(g->iter_ev, &v[PR_STAT_ITER_MS_MEAN]));
+  // an iteration ends when both its kernels (compute stream) and its exchange (xstream, P > 1)
+  // are done: per iteration the later of the two ends, measured from the iteration's start
+  // (the transfer runs on xstream since round 2)
+  if (g->xchg_ev.size() == g->iter_ev.size() && !g->xchg_ev.empty()) {
+    double acc = 0.0;
+    for (size_t i = 0; i < g->iter_ev.size(); ++i) {
+      float a = 0.f, b = 0.f;
+      PR_HIP(hipEventElapsedTime(&a, g->ev_pool[g->iter_ev[i].first], g->ev_pool[g->iter_ev[i].second]));
+      PR_HIP(hipEventElapsedTime(&b, g->ev_pool[g->iter_ev[i].first], g->ev_pool[g->xchg_ev[i].second]));
+      acc += a > b ? a : b;
+    }
+    v[PR_STAT_ITER_MS_MEAN] = acc / (double)g->iter_ev.size();
+  } else {
+    PR_TRY(mean_ms(g->iter_ev, &v[PR_STAT_ITER_MS_MEAN]));
+  }
   v[PR_STAT_BUILD_MS] = g->build_ms;
   PR_TRY(mean_ms(g->xchg_ev, &v[PR_STAT_EXCHANGE_MS_MEAN]));
   for (int32_t i = 0; i < n_stats && i < PR_STAT_COUNT; ++i) stats[i] = v[i];
@@ -354,7 +422,7 @@ static int check_group(pr_graph *const *parts, int32_t n) {
     if (g->nparts != n || g->part != p) return fail(PR_ERR_INVALID, "parts[p] must be part p of n_parts");
     if (g->V != parts[0]->V || g->S_pad != parts[0]->S_pad) return fail(PR_ERR_INVALID, "parts of different graphs");
     if (g->comm) return fail(PR_ERR_STATE, "a part with an RCCL communicator cannot join a group");
-    if (g->x_allgather != parts[0]->x_allgather) return fail(PR_ERR_INVALID, "parts built with different PR_EXCHANGE");
+    if (g->x_allgather != parts[0]->x_allgather) return fail(PR_ERR_INVALID, "parts built with different PR_BOPT_EXCHANGE");
   }
   return PR_OK;
 }

@@ -128,6 +128,16 @@ __global__ void k_reader_est(int32_t V, int P, const int32_t *__restrict__ deg, 
   atomicAdd(sum, acc);
 }
 
+// Out-degree sum of the first n vertices of the degree order (the layout policy's estimate of the
+// in-links the split layout's LDS hot sets would serve).
+__global__ void k_top_degree_sum(int64_t n, int b, uint64_t maxd, const uint64_t *__restrict__ sorted_vk,
+                                 unsigned long long *__restrict__ sum) {
+  unsigned long long acc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc += maxd - (sorted_vk[i] >> b);
+  atomicAdd(sum, acc);
+}
+
 // Internal order key: out-degree descending, original ID ascending (hot contributions first).
 __global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
                              uint64_t *__restrict__ vk) {
@@ -176,6 +186,53 @@ struct PartXform {
     return (seg << (brow + bg)) | (row << bg) | (uint64_t)gs;
   }
 };
+
+// Row-block layout (pr_rows.h): (row << bg) | gather position -> the sweep key
+// (tile, region, row within the tile, position within the region), the position mapped into the
+// compacted gather space first (cmap, P > 1); *bad counts sources the exchange lists miss.
+__global__ void k_rows_rekey(int64_t n, uint64_t *__restrict__ keys, int bg, const int32_t *__restrict__ cmap,
+                             unsigned long long *__restrict__ bad) {
+  constexpr int sh = kRowsRegionShift, bt = kRowsTileBits;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    const uint64_t row = k >> bg;
+    int64_t gs = (int64_t)(k & ((uint64_t(1) << bg) - 1));
+    if (cmap) {
+      gs = cmap[gs];
+      if (gs < 0) {
+        atomicAdd(bad, 1ull);
+        gs = 0;
+      }
+    }
+    const uint64_t tile = row >> bt, rit = row & (kRowsTile - 1);
+    const int bp = bg > sh ? bg : sh;  // position bits (a region may exceed a small gather space)
+    keys[i] = (tile << (bp + bt)) | (((uint64_t)gs >> sh) << (sh + bt)) | (rit << sh) |
+              ((uint64_t)gs & ((uint64_t(1) << sh) - 1));
+  }
+}
+
+// Row-block layout: entry i of the sorted sweep keys -> its code (byte offset | segment end) and row
+// within the tile, at its place in the tile's padded unit stream.  A segment ends where (tile,
+// region, row) changes, at the tile's last entry and at every unit's last entry.
+__global__ void k_rows_fill(int64_t n, const uint64_t *__restrict__ keys, int bg, const int64_t *__restrict__ tile_beg,
+                            const int64_t *__restrict__ tile_u, uint32_t *__restrict__ codes,
+                            uint16_t *__restrict__ rows) {
+  constexpr int sh = kRowsRegionShift, bt = kRowsTileBits;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const int bp = bg > sh ? bg : sh;
+    const int64_t t = (int64_t)(key >> (bp + bt));
+    const int64_t k = i - tile_beg[t];
+    const int64_t p = tile_u[t] * kWaveUnit + k;
+    const uint64_t rit = (key >> sh) & (kRowsTile - 1);
+    const uint64_t pos = (((key >> (sh + bt)) & ((uint64_t(1) << (bp - sh)) - 1)) << sh) |
+                         (key & ((uint64_t(1) << sh) - 1));
+    const bool last = i + 1 == tile_beg[t + 1];
+    const bool end = last || (k % kWaveUnit) == kWaveUnit - 1 || (keys[i + 1] >> sh) != (key >> sh);
+    codes[p] = (uint32_t)(pos * 8) | (end ? 1u : 0u);
+    rows[p] = (uint16_t)rit;
+  }
+}
 
 // row_ptr over rows [0, R) of keys[lo, hi) whose row is (key >> shift) & rmask.
 __global__ void k_row_ptr_seg(const uint64_t *__restrict__ keys, int64_t lo, int64_t hi, int shift,
@@ -335,13 +392,15 @@ __global__ void k_map_cols(int64_t n, const int32_t *__restrict__ cmap, int32_t 
   }
 }
 
-// One workgroup per wave unit: its entry codes (end marks in bit 0, padding 0).
+// One workgroup per wave unit: its entry codes (end marks in bit 0, padding 0); *n_hot counts the
+// entries that read the LDS hot set.
 __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *__restrict__ units,
                                                   const int64_t *__restrict__ src_off,
                                                   const int32_t *__restrict__ n_real,
                                                   const int32_t *__restrict__ col,
                                                   const int32_t *__restrict__ hotidx,
-                                                  uint32_t *__restrict__ colh) {
+                                                  uint32_t *__restrict__ colh, unsigned long long *n_hot) {
+  unsigned long long nh = 0;
   for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
     const Unit u = units[b];
     uint32_t *dst = colh + (int64_t)u.p8 * 8;
@@ -352,78 +411,91 @@ __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *_
       if (i < n) {
         const int32_t v = col[s0 + i];
         c = hot_code(v & 0x7FFFFFFF, hotidx, u.meta >= 0 && v < 0);
+        nh += (c & kEntGlobal) ? 0 : 1;
       }
       dst[i] = c;
     }
   }
+  atomicAdd(n_hot, nh);
 }
 
-// One wave per unit: the lane metadata word (end mask, the static predicates of the segmented
-// scan, the lane's first segment index) from the end marks in bit 0 of the codes, which stay
-// (the kernel masks them).  Only for PR_HOT_META=1: by default k_spmv_hot derives the same word
-// in-kernel (pr_spmv.h derive_meta).
-__global__ __launch_bounds__(64) void k_unit_meta(int64_t n_units, const Unit *__restrict__ units,
-                                                  uint32_t *__restrict__ colh, uint32_t *__restrict__ meta) {
-  const int t = threadIdx.x;
-  for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
-    const Unit u = units[b];
-    uint32_t endm = 0;
-    int excl = 0;
-    uint32_t *c = colh + (int64_t)u.p8 * 8 + t * kWavePT;
-    const bool live = t * kWavePT < u.n;
-    for (int j = 0; j < kWavePT; ++j) {
-      const uint32_t v = live ? c[j] : 0u;
-      const bool e = u.meta >= 0 && (v & 1u);
-      endm |= (e ? 1u : 0u) << j;
-      const unsigned long long bm = __ballot(e);
-      excl += __popcll(bm & lanemask_lt());
-    }
-    const unsigned long long F = __ballot(endm != 0);
-    // no segment end among lanes [lo, t]
-    auto clear = [&](int lo) -> bool {
-      const unsigned long long m = (t == 63 ? ~0ull : ((1ull << (t + 1)) - 1)) & ~((1ull << lo) - 1);
-      return (F & m) == 0;
-    };
-    uint32_t cond = 0;
-    const int r = t & 15, row = t >> 4;
-    for (int s = 0; s < 4; ++s) {
-      const int k = 1 << s;
-      if (r >= k && clear(t - k + 1)) cond |= 1u << s;
-    }
-    if ((row == 1 || row == 3) && clear(row * 16)) cond |= 1u << 4;
-    if (row >= 2 && clear(32)) cond |= 1u << 5;
-    meta[b * 64 + t] = endm | (cond * kMetaStep0) | ((uint32_t)excl << kMetaExclShift);
-  }
-}
-
-// Tuning knobs read at build time.
 // Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the part's
 // gather space (its slice plus the expected received runs at P > 1) fits one XCD's 4 MiB L2 (the
-// phased schedule runs one class per XCD at a time), capped at kAutoMaxClasses; PR_CLASSES
+// phased schedule runs one class per XCD at a time), capped at kAutoMaxClasses; PR_BOPT_CLASSES
 // overrides.  More classes keep more gathers in L2 and the LDS hot sets but cost epilogue work per
 // (row, class): R-MAT s26 (262 MB) -> 64 at P = 1, 2, 4 and 32 for an 8-way part (121 MB: 8 % less
 // per iteration than 64); the Twitter shape stays at 64 at P = 8 (6 % better than 32); ER s24
 // (134 MB) -> 64, LiveJournal (39 MB) -> 16 (profiles/r02/class_policy/).
 constexpr int64_t kClassRegionBytes = 4000000;  // just under the 4 MiB L2: ER s24 (4.19 MB at 32) stays at 64
-static int class_setting(int64_t gather_bytes) {
-  if (const char *e = getenv("PR_CLASSES")) {
-    const int c = atoi(e);
-    return (c == 8 || c == 16 || c == 64 || c == 128) ? c : 32;
-  }
+static int class_setting(const pr_build_opts &o, int64_t gather_bytes) {
+  if (o.classes) return o.classes;
   for (int c = kXcds; c < kAutoMaxClasses; c *= 2)
     if (gather_bytes <= (int64_t)c * kClassRegionBytes) return c;
   return kAutoMaxClasses;
 }
 
-static bool hot_phased_setting() {
-  const char *e = getenv("PR_HOT_PHASED");  // tuning knob
-  return e ? atoi(e) != 0 : true;
+static int hot_slots_setting(const pr_build_opts &o) {
+  const int k = o.hot_slots < 0 ? kHotSlotsDefault : o.hot_slots;
+  return std::max(0, std::min(k, kHotSlotsMax));
 }
 
-static int hot_slots_setting() {
-  int k = kHotSlotsDefault;
-  if (const char *e = getenv("PR_HOT_SLOTS")) k = atoi(e);  // tuning knob
-  return std::max(0, std::min(k, kHotSlotsMax));
+// Row-block layout plan (pr_rows.h): keys hold the part's in-links as (local row << bg) | gather
+// position; re-keyed to (tile, region, row within the tile, position) and sorted, they become
+// every tile's sweep stream, cut into kWaveUnit-entry units padded per tile.
+static int plan_rows(pr_graph *g, uint64_t *keys, uint64_t *tmp, int64_t lm, int bg, const int32_t *cmap) {
+  hipStream_t s = g->stream;
+  const unsigned T = 256;
+  const int64_t nt = (g->n_rows + kRowsTile - 1) / kRowsTile;
+  const int bp = std::max(bg, kRowsRegionShift);  // the sweep key's position bits (k_rows_rekey)
+  g->n_tiles = nt;
+  if (lm > 0) {
+    DevBuf bad;
+    PR_TRY(bad.alloc(sizeof(unsigned long long)));
+    PR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_rows_rekey, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s, lm, keys, bg, cmap,
+                       bad.as<unsigned long long>());
+    PR_HIP(hipGetLastError());
+    unsigned long long hb = 0;
+    PR_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(hb), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
+    if (hb) return fail(PR_ERR_STATE, "exchange lists miss a source of this part's in-links");
+    PR_TRY(radix_sort_u64(keys, tmp, lm, 0, bp + kRowsTileBits + bits_for((uint64_t)nt), s));
+  }
+  DevBuf beg;
+  PR_TRY(beg.alloc(sizeof(int64_t) * (size_t)(nt + 1)));
+  hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s, keys, (int64_t)0, lm,
+                     bp + kRowsTileBits, ~uint64_t(0), nt, beg.as<int64_t>());
+  PR_HIP(hipGetLastError());
+  std::vector<int64_t> hb((size_t)nt + 1), hu((size_t)nt + 1);
+  PR_HIP(hipMemcpyAsync(hb.data(), beg.p, sizeof(int64_t) * hb.size(), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  int64_t nu = 0;
+  for (int64_t t = 0; t < nt; ++t) {
+    hu[t] = nu;
+    nu += (hb[t + 1] - hb[t] + kWaveUnit - 1) / kWaveUnit;
+  }
+  hu[nt] = nu;
+  g->n_runits = nu;
+  PR_TRY(g->tile_u.alloc(sizeof(int64_t) * hu.size()));
+  PR_HIP(hipMemcpyAsync(g->tile_u.p, hu.data(), sizeof(int64_t) * hu.size(), hipMemcpyHostToDevice, s));
+  const int64_t ne = nu * kWaveUnit;
+  PR_TRY(g->rcodes.alloc(sizeof(uint32_t) * (size_t)(ne > 0 ? ne : 1)));
+  PR_TRY(g->rrows.alloc(sizeof(uint16_t) * (size_t)(ne > 0 ? ne : 1)));
+  // padding: an out-of-range offset (no memory request) without an end mark, row 0
+  PR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->rcodes.p), 0xFFFFFFF0u, (size_t)(ne > 0 ? ne : 1), s));
+  PR_HIP(hipMemsetAsync(g->rrows.p, 0, sizeof(uint16_t) * (size_t)(ne > 0 ? ne : 1), s));
+  if (lm > 0)
+    hipLaunchKernelGGL(k_rows_fill, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s, lm, keys, bg, beg.as<int64_t>(),
+                       g->tile_u.as<int64_t>(), g->rcodes.as<uint32_t>(), g->rrows.as<uint16_t>());
+  PR_HIP(hipGetLastError());
+  int n_cu = 0;
+  PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
+  g->rows_grid = std::max(1, n_cu * kRowsWgPerCu);
+  const int64_t waves = (int64_t)g->rows_grid * kRowsWaves;
+  g->rows_passes = (int)std::max<int64_t>(1, (nt + waves - 1) / waves);
+  PR_TRY(prepare_hot_kernel());
+  PR_HIP(hipStreamSynchronize(s));
+  return PR_OK;
 }
 
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
@@ -532,18 +604,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     gather_est += (int64_t)((double)est / 1048576.0 * (double)(P - 1) / (double)P) * 8;
   }
   g->gather_est = gather_est;
-  const int c_split = class_setting(gather_est);
-  int C = ((int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes) ? c_split : 1;
-  if (g->flags & PR_LAYOUT_FUSED) C = 1;
-  if (g->flags & PR_LAYOUT_SPLIT) C = c_split;
-  // heavy-row entry codes are byte offsets below 2^31 (pr_internal.h)
-  if ((int64_t)P * (g->n_local_max + 64 + kMaxClasses) * 8 >= (1ll << 31) - (1ll << 20)) C = 1;
-  g->C = C;
-  g->Q_pad = (g->n_local_max + C - 1) / C;
-  g->Q_pad = (g->Q_pad + 63) / 64 * 64;  // rows come in whole 64-row blocks (k_epilogue)
-  g->n_rows = (int64_t)C * g->Q_pad;
-  g->S_pad = ((g->n_rows + 2 + 63) / 64) * 64;
-  if ((int64_t)P * g->S_pad >= (int64_t(1) << 31)) return fail(PR_ERR_INVALID, "gather space exceeds 2^31 entries");
   const int bd = bits_for(max_outdeg);
   const uint64_t maxd = (uint64_t(1) << bd) - 1;
   DevBuf vk, vtmp, rank_of, gpos;
@@ -555,11 +615,44 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hipLaunchKernelGGL(k_order_keys, dim3(grid_for(V, T, 4096)), dim3(T), 0, s, V, b, maxd, c_deg.as<int32_t>(),
                        vk.as<uint64_t>());
     PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd, s));
+  }
+  vtmp.reset();
+  // Layout policy: the fused layout while the gather space fits the L2s; beyond, the split layout
+  // (column classes with LDS hot sets) unless its hot sets would serve fewer than kRowsMaxHotCover
+  // of the in-links (uniform graphs) -- then the row-block layout, which keeps row sums in LDS and
+  // writes no partial slots.  The hot sets hold the top c_split * slots sources of the degree order.
+  const int c_split = class_setting(g->opts, gather_est);
+  const bool big = (int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes;
+  int layout = big ? kLayoutSplit : kLayoutFused;
+  if (kRowsMaxHotCover > 0.0 && big && !(g->flags & (PR_LAYOUT_SPLIT | PR_LAYOUT_FUSED)) && m > 0) {
+    const int64_t n_hot = std::min<int64_t>(V, (int64_t)c_split * hot_slots_setting(g->opts));
+    PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_top_degree_sum, dim3(grid_for(n_hot, T, 1024)), dim3(T), 0, s, n_hot, b, maxd,
+                       vk.as<uint64_t>(), cnt.as<unsigned long long>());
+    PR_HIP(hipGetLastError());
+    unsigned long long top = 0;
+    PR_HIP(hipMemcpyAsync(&top, cnt.p, sizeof(top), hipMemcpyDeviceToHost, s));
+    PR_HIP(hipStreamSynchronize(s));
+    if ((double)top < kRowsMaxHotCover * (double)m) layout = kLayoutRows;
+  }
+  if (g->flags & PR_LAYOUT_FUSED) layout = kLayoutFused;
+  if (g->flags & PR_LAYOUT_SPLIT) layout = kLayoutSplit;
+  if (g->flags & PR_LAYOUT_ROWS) layout = kLayoutRows;
+  // split and row-block entry codes are byte offsets below 2^31 (pr_internal.h)
+  if ((int64_t)P * (g->n_local_max + 64 + kMaxClasses) * 8 >= (1ll << 31) - (1ll << 20)) layout = kLayoutFused;
+  int C = layout == kLayoutSplit ? c_split : 1;
+  g->layout = layout;
+  g->C = C;
+  g->Q_pad = (g->n_local_max + C - 1) / C;
+  g->Q_pad = (g->Q_pad + 63) / 64 * 64;  // rows come in whole 64-row blocks (k_epilogue_grp)
+  g->n_rows = (int64_t)C * g->Q_pad;
+  g->S_pad = ((g->n_rows + 2 + 63) / 64) * 64;
+  if ((int64_t)P * g->S_pad >= (int64_t(1) << 31)) return fail(PR_ERR_INVALID, "gather space exceeds 2^31 entries");
+  if (V > 0) {
     hipLaunchKernelGGL(k_rank_gpos, dim3(grid_for(V, T, 65536)), dim3(T), 0, s, V, maskb, P, C,
                        g->Q_pad, g->S_pad, vk.as<uint64_t>(), rank_of.as<int32_t>(), gpos.as<int32_t>());
     PR_HIP(hipGetLastError());
   }
-  vtmp.reset();
   ClassGeom geo{};
   geo.C = C;
   geo.Q_pad = g->Q_pad;
@@ -568,7 +661,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
 
   // ---- exchange lists (P > 1): which of this part's contributions every peer reads ----
   DevBuf cmap;  // global -> compacted gather position (P > 1, sparse exchange)
-  g->hot_phased = C > 1 && hot_phased_setting();  // the exchange is chunked by hot phase
   PR_TRY(build_exchange(g, ukeys, m, b, maskb, rank_of.as<int32_t>(), gpos.as<int32_t>(), &cmap));
 
   // ---- the part's in-link CSRs: one per column class (one in the fused layout) ----
@@ -583,11 +675,11 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                        keys.as<uint64_t>(), &lm, s));
   g->local_nnz = lm;
   PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, 0, bg + brow + bseg, s));
-  PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 ? lm : 1)));
-  if (lm > 0)
+  PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 && layout != kLayoutRows ? lm : 1)));
+  if (lm > 0 && layout != kLayoutRows)
     hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
                        keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
-  if (cmap.p && lm > 0) {  // columns -> the compacted gather space (order within rows kept)
+  if (cmap.p && lm > 0 && layout != kLayoutRows) {  // columns -> the compacted gather space (order within rows kept)
     DevBuf bad;
     PR_TRY(bad.alloc(sizeof(unsigned long long)));
     PR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
@@ -619,7 +711,12 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   int64_t pieces = 0;
   g->nblk = (R + 63) / 64;
   std::vector<int64_t> poff(kMaxClasses + 1, 0);
-  if (C == 1) {
+  if (layout == kLayoutRows) {
+    PR_TRY(plan_rows(g, keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, bg, cmap.p ? cmap.as<int32_t>() : nullptr));
+    keys.reset();
+    tmp.reset();
+    seg_p0.push_back(0);
+  } else if (C == 1) {
     // fused layout: one CSR over all rows, 256-thread units with the fused epilogue
     DevBuf rp_dev;
     PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
@@ -653,20 +750,11 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     for (int x = C; x < kMaxClasses; ++x) poff[x + 1] = poff[x];
     for (int x = 0; x < C; ++x)
       if (poff[x + 1] - poff[x] >= (int64_t(1) << 29)) return fail(PR_ERR_INVALID, "a column class exceeds 2^29 segments");
-    // k_epilogue<C, true>: one buffer resource over all partials, so every partial needs a 32-bit
-    // byte offset (< 2^29 slots).  k_epilogue_grp addresses partials through int32 absolute slot
-    // indices (< 2^31 slots: R-MAT s26 has ~2^28.1, a graph 7x its size still fits).
-    g->epi_abs = poff[C] < (int64_t(1) << 29) - 1;
-    if (const char *e = getenv("PR_EPI_ABS")) g->epi_abs = g->epi_abs && atoi(e) != 0;  // A/B knob
-    g->epi_grp = poff[C] < (int64_t(1) << 31) - 4;
-    if (const char *e = getenv("PR_EPI_GRP")) g->epi_grp = g->epi_grp && atoi(e) != 0;  // A/B knob
-    if (C > 32 && !g->epi_grp) return fail(PR_ERR_INVALID, "more than 32 column classes need the grouped epilogue (< 2^31 partial slots)");
-    if (!g->epi_grp && !g->epi_abs && poff[C] >= (int64_t(1) << 31) - 4)
-      return fail(PR_ERR_INVALID, "more than 2^31 partial slots");
-    if (const char *e = getenv("PR_EPI_VAR")) g->epi_var = std::min(std::max(atoi(e), 0), kNumEpiVariants - 1);
-    // per-block first slots: absolute (grouped epilogue, k_epilogue<C, true>) or class-local,
-    // plus the sentinel block row of every class's end slot
-    PR_TRY(sp.block_bases(g->epi_abs || g->epi_grp, s));
+    // k_epilogue_grp addresses partials through int32 absolute slot indices (< 2^31 slots: R-MAT
+    // s26 has ~2^28.1, the Twitter shape ~2^29; a graph several times their size still fits)
+    if (poff[C] >= (int64_t(1) << 31) - 4) return fail(PR_ERR_INVALID, "more than 2^31 - 4 partial slots");
+    // per-block first slots (absolute), plus the sentinel block row of every class's end slot
+    PR_TRY(sp.block_bases(true, s));
     PR_TRY(sp.units_plan(s));
     g->rmask = std::move(sp.rmask);
     g->cbase = std::move(sp.cbase);
@@ -674,7 +762,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     pieces = sp.n_pieces;
     if (sp.entries / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
     // LDS hot set per class, then the entry codes
-    const int slots = hot_slots_setting();
+    const int slots = hot_slots_setting(g->opts);
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
@@ -682,10 +770,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
-    // units reach waves through the workgroup's LDS counter: -3.5 % at s26, -0.7..-2.3 % per part
-    // at P = 2 / 8, -0.8 % at ER s24 against the static interleave (profiles/r02/assign_lds_ab/)
-    hg.assign = 3;
-    if (const char *e = getenv("PR_HOT_ASSIGN")) hg.assign = std::min(3, std::max(0, atoi(e)));
     g->hot = hg;
     // hot-set gather positions per class, and the LDS slot of every hot gather position
     DevBuf hotidx;
@@ -699,12 +783,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipGetLastError());
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
-    int wg_per_cu = 1;  // A/B knob: co-resident k_spmv_hot workgroups per CU (needs PR_HOT_SLOTS small enough)
-    if (const char *e = getenv("PR_HOT_WGS_PER_CU")) wg_per_cu = std::min(std::max(atoi(e), 1), 4);
-    g->hot_grid = std::max(C, n_cu * wg_per_cu / C * C);  // C | grid: every class gets the same CUs
+    g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
     g->hot_grid_full = g->hot_grid;
-    g->hot_phased = hot_phased_setting();
-    if (const char *e = getenv("PR_HOT_RESERVE")) PR_TRY(set_hot_reserve(g, atoi(e)));  // A/B knob
+    PR_TRY(set_hot_reserve(g, g->opts.hot_reserve));
 
     PR_TRY(prepare_hot_kernel());
     const int64_t nu = sp.n_units;
@@ -713,23 +794,21 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
-    if (const char *e = getenv("PR_HOT_META")) g->hot_meta = atoi(e) != 0;  // A/B knob
-    PR_TRY(g->hmeta.alloc(g->hot_meta ? sizeof(uint32_t) * kWave * (nu + 1) : 8));
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
     g->n_slots = poff[C];
-    for (int x = 0; x <= kMaxClasses; ++x) g->part_off.o[x] = poff[x];
     PR_HIP(hipMemcpyAsync(g->hucum.p, sp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     if (nu > 0) {
+      PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), s));
       hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
                          g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
-                         hotidx.as<int32_t>(), g->colh.as<uint32_t>());
-      if (g->hot_meta)
-        hipLaunchKernelGGL(k_unit_meta, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(kWave), 0, s, nu,
-                           g->hunits.as<Unit>(), g->colh.as<uint32_t>(), g->hmeta.as<uint32_t>());
+                         hotidx.as<int32_t>(), g->colh.as<uint32_t>(), cnt.as<unsigned long long>());
       PR_HIP(hipGetLastError());
+      unsigned long long n_hot = 0;
+      PR_HIP(hipMemcpyAsync(&n_hot, cnt.p, sizeof(n_hot), hipMemcpyDeviceToHost, s));
       PR_HIP(hipStreamSynchronize(s));
+      g->hot_cover_ppm = lm > 0 ? (int64_t)((double)n_hot * 1e6 / (double)lm) : 0;
     }
     g->n_segs = sp.n_long;
     g->seg_slot = std::move(sp.seg_slot);
@@ -773,22 +852,19 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   PR_TRY(g->fin_counter.alloc(sizeof(unsigned) * 4));
   PR_HIP(hipMemsetAsync(g->fin_counter.p, 0, sizeof(unsigned) * 4, s));
   g->reset_blocks = (int)grid_for(g->n_rows > 0 ? g->n_rows : 1, 256, 2048);
-  if (C > 1 && g->epi_grp) {
+  if (C > 1) {
     // one wave per group, no grid cap: the whole grid in one dispatch lets the workgroups of the
     // last round finish together (R-MAT s26: 16 K workgroups, -1.8 % per step against a 2048 cap
-    // whose waves stride over 8 groups; profiles/r02/experiments.md)
-    int cap = 1 << 20;
-    if (const char *e = getenv("PR_EPI_BLOCKS")) cap = std::max(atoi(e), 1);  // A/B knob
-    // one-wave workgroups pay off when many groups walk (a cheap group's wave frees its LDS
-    // window at once: R-MAT s26 -0.8 %), four-wave ones on uniform graphs (ER s24 +1.3 % narrow)
-    const int64_t ngrp = (g->nblk + kEpiVariants[g->epi_var].G - 1) / kEpiVariants[g->epi_var].G;
-    g->epi_narrow = epi_narrow_ok(g->epi_var) && g->n_walk_groups * 10 >= ngrp;
-    if (const char *e = getenv("PR_EPI_NARROW")) g->epi_narrow = epi_narrow_ok(g->epi_var) && atoi(e) != 0;  // A/B
-    g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_var, g->epi_narrow) / kWave, cap);
+    // whose waves stride over 8 groups; profiles/r02/experiments.md).  One-wave workgroups pay off
+    // when many groups walk (a cheap group's wave frees its LDS window at once: R-MAT s26 -0.8 %),
+    // four-wave ones on uniform graphs (ER s24 +1.3 % narrow); at most 64 classes
+    const int64_t ngrp = (g->nblk + kEpiGroup - 1) / kEpiGroup;
+    const bool auto_narrow = g->n_walk_groups * 10 >= ngrp;
+    g->epi_narrow = epi_narrow_ok(C) && (g->opts.epi_narrow < 0 ? auto_narrow : g->opts.epi_narrow != 0);
+    g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
   }
-  else
-    g->ep_blocks = C > 1 ? (int)grid_for(g->nblk > 0 ? g->nblk : 1, kThreads / kWave, 2048) : 0;
-  // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
+  if (layout == kLayoutRows) g->ep_blocks = g->rows_grid * g->rows_passes;  // k_spmv_rows' block partials
+  // finalize input: fused-unit partials, the split epilogue's or the row-block passes' block partials
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 

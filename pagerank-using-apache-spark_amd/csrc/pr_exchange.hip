@@ -11,7 +11,7 @@
 // At R-MAT s26 with 8 parts each rank receives 39 % of what an all-gather of whole slices moves.
 //
 // Transport: RCCL grouped ncclSend / ncclRecv (one process per GPU), or device-to-device copies
-// (pr_group_*: one process, several parts).  PR_EXCHANGE=allgather restores whole slices in an
+// (pr_group_*: one process, several parts).  PR_BOPT_EXCHANGE = 1 restores whole slices in an
 // uncompacted gather space of P slices (A/B, diagnostics).
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +19,7 @@
 #include "pr_compact.h"
 #include "pr_device.h"
 #include "pr_graph.h"
+#include "pr_xcheck.h"
 
 namespace pr {
 namespace {
@@ -166,11 +167,6 @@ int chunk_bounds(pr_graph *g, const uint32_t *list, const std::vector<int64_t> &
   return PR_OK;
 }
 
-bool allgather_requested() {
-  const char *e = getenv("PR_EXCHANGE");
-  return e && std::strcmp(e, "allgather") == 0;
-}
-
 // One direction's list (send or receive) of part g->part.
 int build_list(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
                const int32_t *gpos, bool send, DevBuf *list, std::vector<int64_t> *off) {
@@ -219,7 +215,7 @@ double *send_runs(const pr_graph *g, int buf) {
 int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
                    const int32_t *gpos, DevBuf *cmap) {
   const int P = g->nparts, self = g->part;
-  g->x_allgather = P > 1 && allgather_requested();
+  g->x_allgather = P > 1 && g->opts.allgather;
   g->slots.n = P;
   if (P <= 1 || g->x_allgather) {  // P slices side by side
     g->gsize = (int64_t)P * g->S_pad;
@@ -251,7 +247,7 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   PR_HIP(hipStreamSynchronize(s));
   // chunk bounds of the overlapped exchange: one chunk per hot phase (whether the chunks travel
   // separately: x_chunked, PR_XCHG_CHUNKS / pr_set_option)
-  g->n_xc = (g->C > 1 && g->hot_phased) ? std::max(1, g->C / kXcds) : 1;
+  g->n_xc = g->C > 1 ? std::max(1, g->C / kXcds) : 1;
   set_exchange_chunking(g);
   PR_TRY(chunk_bounds(g, g->x_send.as<uint32_t>(), g->x_soff, true, &g->x_sch));
   PR_TRY(chunk_bounds(g, recv.as<uint32_t>(), g->x_roff, false, &g->x_rch));
@@ -271,29 +267,15 @@ int exchange_pack(pr_graph *g, int buf) {
   return PR_OK;
 }
 
-// After ncclCommInitRank: every rank publishes {graph shape, exchange mode, its send-run lengths,
-// their chunk sizes} and checks that what each peer sends it is exactly what it expects to
-// receive, chunk by chunk, so a mismatch (different inputs, different PR_EXCHANGE /
-// PR_XCHG_CHUNKS / PR_HOT_PHASED per rank) fails loudly at attach time instead of desynchronising
-// the send/receive pairs.  The record has the same length on every rank (kMaxChunks slots per peer).
+// After ncclCommInitRank: every rank publishes its exchange record (pr_xcheck.h) and checks every
+// peer's against what it expects to receive, chunk by chunk; a mismatch fails loudly at attach
+// time (or at pr_set_option) instead of desynchronising the send/receive pairs.
 int verify_exchange(pr_graph *g) {
-  constexpr int kMaxChunks = kMaxClasses / kXcds;
   const int P = g->nparts, nc = g->n_xc;
-  if (nc > kMaxChunks) return fail(PR_ERR_INVALID, "too many exchange chunks");
-  const int CH = P + 4;  // chunk sizes start here: [CH + q * kMaxChunks + c]
-  const int W = CH + P * kMaxChunks;
+  const int W = xrec_width(P);
   std::vector<int64_t> mine(W, 0);
-  mine[0] = g->V;
-  mine[1] = g->S_pad;
-  mine[2] = g->x_allgather ? 1 : 0;
-  // chunking of the overlapped exchange: the grouped send/recv calls of every chunk must pair up
-  mine[P + 3] = 2 * (int64_t)nc + (g->x_chunked ? 1 : 0);
-  if (!g->x_allgather)
-    for (int q = 0; q < P; ++q) {
-      mine[3 + q] = g->x_soff[q + 1] - g->x_soff[q];
-      for (int c = 0; c < nc; ++c)
-        mine[CH + q * kMaxChunks + c] = g->x_sch[(size_t)q * (nc + 1) + c + 1] - g->x_sch[(size_t)q * (nc + 1) + c];
-    }
+  if (!xrec_fill(g->V, g->S_pad, g->x_allgather, nc, g->x_chunked, P, g->x_soff.data(), g->x_sch.data(), mine.data()))
+    return fail(PR_ERR_INVALID, "too many exchange chunks");
   DevBuf d;
   PR_TRY(d.alloc(sizeof(int64_t) * (size_t)W * (P + 1)));
   PR_HIP(hipMemcpyAsync(d.as<int64_t>(), mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, g->stream));
@@ -302,19 +284,9 @@ int verify_exchange(pr_graph *g) {
   std::vector<int64_t> all((size_t)W * P);
   PR_HIP(hipMemcpyAsync(all.data(), d.as<int64_t>() + W, sizeof(int64_t) * W * P, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
-  const int me = g->part;
-  for (int q = 0; q < P; ++q) {
-    const int64_t *o = all.data() + (size_t)q * W;
-    if (o[0] != g->V || o[1] != g->S_pad) return fail(PR_ERR_INVALID, "ranks hold parts of different graphs");
-    if (o[2] != mine[2]) return fail(PR_ERR_INVALID, "ranks disagree on PR_EXCHANGE");
-    if (o[P + 3] != mine[P + 3]) return fail(PR_ERR_INVALID, "ranks disagree on the exchange chunking");
-    if (q == me || g->x_allgather) continue;
-    if (o[3 + me] != g->x_roff[q + 1] - g->x_roff[q]) return fail(PR_ERR_STATE, "exchange lists disagree between ranks");
-    for (int c = 0; c < nc; ++c)
-      if (o[CH + me * kMaxChunks + c] != g->x_rch[(size_t)q * (nc + 1) + c + 1] - g->x_rch[(size_t)q * (nc + 1) + c])
-        return fail(PR_ERR_STATE, "exchange chunks disagree between ranks");
-  }
-  return PR_OK;
+  const char *why = "";
+  const int rv = xrec_check(all.data(), P, g->part, mine.data(), g->x_roff.data(), g->x_rch.data(), nc, &why);
+  return rv == PR_OK ? PR_OK : fail(rv, why);
 }
 
 // One process per GPU (RCCL).  Whole slices: one in-place ncclAllGather on the compute stream.

@@ -7,7 +7,7 @@
 //   slice                   S_pad doubles per part: the contributions c = r/d of its rows, then
 //                           two slots {dangling partial, L1 partial}.
 //   gather space (cbuf)     what this part's in-links read: P slices side by side (P = 1,
-//                           PR_EXCHANGE=allgather), or - the default for P > 1 - this part's
+//                           PR_BOPT_EXCHANGE = 1), or - the default for P > 1 - this part's
 //                           slice followed by the runs it receives from every peer (only the
 //                           sources of its own in-links; pr_exchange.hip).  Double-buffered.
 //   rowinfo uint32[R]         out-degree | kRowSink (in D) | kRowIndeg0 | kRowHole
@@ -31,17 +31,30 @@
 
 #include "pr_internal.h"
 
+// Build options (include/pagerank_hip.h PR_BOPT_*): the library reads no environment variables.
+struct pr_build_opts {
+  int classes = 0;       // 0: the size policy
+  int hot_slots = -1;    // -1: kHotSlotsDefault
+  bool allgather = false;
+  bool xchg_chunks = false;
+  int hot_reserve = 0;
+  bool epi_walk = true;
+  int epi_narrow = -1;   // -1: by the share of walking groups
+};
+
 struct pr_graph {
   int device = 0;
   hipStream_t stream = nullptr;
   uint32_t flags = 0;
+  pr_build_opts opts;
 
   int32_t V = 0;          // N = totalUrlCount
   int64_t E_dedup = 0;    // E'
   int part = 0, nparts = 1;
   int64_t n_local = 0;      // rows owned (without holes)
   int64_t n_rows = 0;       // C * Q_pad local rows (with holes)
-  int C = 1;                // column classes
+  int layout = 0;           // pr::kLayoutFused / kLayoutSplit / kLayoutRows
+  int C = 1;                // column classes (split layout; 1 otherwise)
   int64_t gather_est = 0;   // expected gather-space bytes the class count was chosen from
   int64_t Q_pad = 0;        // rows per class region
   int64_t n_local_max = 0;  // ceil(V / P)
@@ -63,25 +76,25 @@ struct pr_graph {
   // per row the mask of classes with in-links (rmask) and per class the slot of the first
   // segment of every 64-row block (cbase[blk][x]); long segments: pieces reduced in order into
   // partial[seg_slot[q]]; hpos[x * P*Kp + i]: gather position of LDS hot slot 1 + i of class x
-  pr::DevBuf colh, hmeta, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
+  pr::DevBuf colh, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};
   int hot_grid = 0;       // workgroups of k_spmv_hot (a multiple of C: one per CU)
   int hot_grid_full = 0;  // the same without reserved CUs (PR_OPT_HOT_RESERVE)
-  bool hot_phased = false;  // an XCD's classes one after another (k_spmv_hot PHASED)
-  bool hot_meta = false;    // lane metadata precomputed in hmeta (PR_HOT_META=1) instead of derived in-kernel
-  bool epi_abs = false;     // cbase holds absolute slots (< 2^29 in total): k_epilogue<C, true>
-  bool epi_grp = false;     // epi_abs + a sentinel cbase row: k_epilogue_grp (LDS-staged class runs)
-  int epi_var = 0;          // its (group, window) variant, pr_spmv.h kEpiVariants (PR_EPI_VAR)
-  // per-row walk in k_epilogue_grp (PR_EPI_WALK): per group the first of its u16 slot positions
-  // in epos, or -1 for the class loop (eoff, i64)
+  // per-row walk in k_epilogue_grp (PR_BOPT_EPI_WALK): per group the first of its u16 slot
+  // positions in epos, or -1 for the class loop (eoff, i64)
   bool epi_walk = false;
-  bool epi_narrow = false;  // one-wave epilogue workgroups (PR_EPI_NARROW; default: many walking groups)
+  bool epi_narrow = false;  // one-wave epilogue workgroups (PR_BOPT_EPI_NARROW; default: many walking groups)
   int64_t n_walk_groups = 0;
   pr::DevBuf eoff, epos;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
-  pr::PartOff part_off{};  // host copy of poff, passed to k_epilogue by value
+  int64_t hot_cover_ppm = 0;  // in-links whose source is in a class's hot set (layout policy input)
+  // row-block layout (pr_rows.h): per tile its first unit (tile_u[n_tiles] = all units), per
+  // entry its code and row within the tile (kWaveUnit entries per unit, padded per tile)
+  pr::DevBuf tile_u, rcodes, rrows;
+  int64_t n_tiles = 0, n_runits = 0;
+  int rows_grid = 0, rows_passes = 0;
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;
@@ -103,7 +116,7 @@ struct pr_graph {
   std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;  // indices into ev_pool
   size_t ev_next = 0;
 
-  // gather space (doubles per cbuf): P slices side by side (P = 1, PR_EXCHANGE=allgather), or
+  // gather space (doubles per cbuf): P slices side by side (P = 1, PR_BOPT_EXCHANGE = 1), or
   // compacted: this part's slice, then the runs received from every peer in peer order
   int64_t gsize = 0;
   int64_t own_off = 0;  // this part's slice in the gather space
@@ -113,7 +126,7 @@ struct pr_graph {
   // (received runs land at S_pad + x_roff[p]), and the double-buffered packed send runs
   pr::DevBuf x_send, x_sbuf;
   std::vector<int64_t> x_soff, x_roff;
-  bool x_allgather = false;  // PR_EXCHANGE=allgather: whole slices instead
+  bool x_allgather = false;  // PR_BOPT_EXCHANGE = 1: whole slices instead
   // Overlapped exchange (P > 1, split layout, phased k_spmv_hot): every peer's run is sent in
   // n_xc chunks on xstream, chunk c = its positions in the class regions of hot phase c (classes
   // [8c, 8c + 8)), the last chunk also carrying the two slots (a run is sorted by position, so
@@ -122,7 +135,7 @@ struct pr_graph {
   // the next iteration's phase c waits for x_ev[c] only (pr_iter.hip), so the transfer of the
   // later classes overlaps the SpMV of the earlier ones.
   int n_xc = 1;
-  // whether the chunks travel separately (PR_XCHG_CHUNKS at build, pr_set_option later);
+  // whether the chunks travel separately (PR_BOPT_XCHG_CHUNKS at build, pr_set_option later);
   // otherwise whole runs, and the next iteration waits for all of them
   bool x_chunked = false;
   std::vector<int64_t> x_sch, x_rch;
@@ -149,10 +162,10 @@ int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);
 int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange
-// x_chunked from PR_XCHG_CHUNKS (1: the overlapped exchange; unset or 0: whole runs, the next
-// iteration waits for all of them).  Off by default: the transfers are kernels (RCCL, blit
-// copies) that compete with k_spmv_hot for CUs -- k_spmv_hot takes a CU's whole LDS, so the two
-// cannot share one -- and on one GPU the chunked group ran 8 % slower.
+// x_chunked from the build option (1: the overlapped exchange; 0: whole runs, the next iteration
+// waits for all of them).  Off by default: the transfers are kernels (RCCL, blit copies) that
+// compete with k_spmv_hot for CUs -- k_spmv_hot takes a CU's whole LDS, so the two cannot share
+// one -- and on one GPU the chunked group ran 8 % slower.
 void set_exchange_chunking(pr_graph *g);
 int n_hot_phases(const pr_graph *g);
 // k_spmv_hot leaves `per_xcd` CUs of every XCD free (phased schedule only: its grid need only be

@@ -72,6 +72,11 @@ inline unsigned grid_for(int64_t n, int threads, unsigned cap = 1u << 20) {
   return (unsigned)g;
 }
 
+// ---- layouts (pr_graph.h) -----------------------------------------------------------------------
+constexpr int kLayoutFused = 0;  // one class, k_spmv_units (gather space <= 4 MiB)
+constexpr int kLayoutSplit = 1;  // column classes, LDS hot sets, partial slots (k_spmv_hot + k_epilogue_grp)
+constexpr int kLayoutRows = 2;   // row tiles with LDS row sums (k_spmv_rows)
+
 // ---- SpMV work plan ------------------------------------------------------------------------
 // A unit is one workgroup of the SpMV launch.  STREAM: whole rows [r0, r0+meta) whose in-links
 // total n <= kUnitNnz.  PIECE: n <= kUnitNnz in-links of one long row r0; meta = -(piece+1).
@@ -94,7 +99,7 @@ __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
 constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
 constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
-constexpr int kMaxClasses = 128;                     // 8, 16, 32, 64 or 128 at run time (PR_CLASSES)
+constexpr int kMaxClasses = 128;                     // 8, 16, 32, 64 or 128 (PR_BOPT_CLASSES)
 constexpr int kAutoMaxClasses = 64;                  // the most the size policy picks by itself
 // per-row class mask (rmask): ceil(C / 32) 32-bit words per row, class x in bit x % 32 of word
 // x / 32 (at 64 classes the two words are one little-endian u64)
@@ -105,24 +110,13 @@ constexpr int64_t kSplitMinSliceBytes = 4ll << 20;
 // Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
-constexpr int kEpiWin = 1024;         // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
-#ifndef PR_EPI_THREADS
-#define PR_EPI_THREADS 256  // other values: A/B builds only (-DPR_EPI_THREADS=...)
-#endif
-constexpr int kEpiThreads = PR_EPI_THREADS;  // 4 waves, 32.1 KiB of LDS: four workgroups per CU
+constexpr int kEpiWin = 1024;  // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
+constexpr int kEpiThreads = 256;  // 4 waves, 32.1 KiB of LDS: four workgroups per CU
 // narrow grouped epilogue: one-wave workgroups (8.2 KiB of LDS each), so a wave that finishes a
 // cheap group frees its window at once -- chosen when a graph has many walking (sparse) groups
 constexpr int kEpiThreadsNarrow = 64;  // one wave64
-// (group, window) variants; PR_EPI_VAR picks one (A/B), 0 is the default
-struct EpiVariant {
-  int G, W;
-  bool legacy = false;  // round-1 staging loop (per-class fill accounting) instead of the prefix batches
-};
-inline bool epi_narrow_ok(int var) { return var == 0; }  // one-wave workgroups: variant 0 only
-inline int epi_grp_threads(int var, bool narrow) { return narrow && epi_narrow_ok(var) ? kEpiThreadsNarrow : kEpiThreads; }
-constexpr EpiVariant kEpiVariants[] = {{kEpiGroup, kEpiWin}, {8, 2048}, {4, 512}, {8, 640}, {16, 1280}, {8, 1016},
-                                       {kEpiGroup, kEpiWin, true}, {8, 1272}};
-constexpr int kNumEpiVariants = sizeof(kEpiVariants) / sizeof(kEpiVariants[0]);
+inline bool epi_narrow_ok(int C) { return C <= 64; }  // one-wave workgroups: at most 64 classes
+inline int epi_grp_threads(bool narrow) { return narrow ? kEpiThreadsNarrow : kEpiThreads; }
 
 // per-row info word: out-degree | flags
 constexpr uint32_t kRowDegMask = (1u << 28) - 1;
@@ -138,8 +132,7 @@ constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
 //   bit 31 clear  LDS byte address of a hot-set slot; slot 0 (address 0) holds 0.0
 //   bit 0         set on the last entry of a segment (both kinds are multiples of 8 otherwise)
 // Padding entries are 0 -- also what a range-checked load past the unit returns.  k_spmv_hot
-// derives its lane metadata from the end marks (pr_spmv.h derive_meta); with PR_HOT_META=1 the
-// build precomputes it instead, one word per unit and lane (hmeta):
+// derives a per-lane metadata word from the end marks (pr_spmv.h derive_meta):
 //   bits 0-7   which of the lane's entries end a segment (STREAM)
 //   bits 8-13  the six partner-add predicates of the wave's segmented scan (pr_spmv.h)
 //   bits 14-23 segment index of the lane's first end within the unit
@@ -153,23 +146,38 @@ constexpr int kMetaExclShift = 14;
 // LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part),
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
 // ~0.5 % and 64 by ~0.8 % at R-MAT s26, profiles/r01/stage_ab/).
-#ifndef PR_STAGE_SLOTS
-#define PR_STAGE_SLOTS 128  // other values: A/B builds only (-DPR_STAGE_SLOTS=...)
-#endif
-constexpr int kStageSlots = PR_STAGE_SLOTS;
+constexpr int kStageSlots = 128;
 constexpr int kHotLdsBytes = 160 * 1024;
 constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 2;
 constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18430 hot contributions (144 KiB)
+
+// ---- row-block layout (pr_rows.h k_spmv_rows) ---------------------------------------------------
+// A tile of kRowsTile local rows belongs to one wave for a pass; its row sums live in LDS.
+// (PR_ROWS_TILE_BITS / PR_ROWS_REGION_SHIFT: -D overrides for A/B builds of the library only)
+#ifndef PR_ROWS_TILE_BITS
+#define PR_ROWS_TILE_BITS 10
+#endif
+#ifndef PR_ROWS_REGION_SHIFT
+#define PR_ROWS_REGION_SHIFT 17
+#endif
+constexpr int kRowsTileBits = PR_ROWS_TILE_BITS;
+constexpr int kRowsTile = 1 << kRowsTileBits;   // rows per tile (8 KiB of fp64 sums)
+constexpr int kRowsWaves = 16;                  // waves per workgroup
+constexpr int kRowsThreads = kRowsWaves * 64;
+constexpr int kRowsRegionShift = PR_ROWS_REGION_SHIFT;  // sweep regions of 2^17 contributions (1 MiB)
+constexpr int kRowsLdsBytes = 8 * kRowsWaves * kRowsTile + 16 * kRowsWaves;
+// workgroups per CU: as many as the LDS holds, at most two (32 waves per CU)
+constexpr int kRowsWgPerCu = (160 * 1024) / kRowsLdsBytes >= 2 ? 2 : 1;
+// the layout policy would route a graph to the row-block layout when the split layout's LDS hot
+// sets serve fewer than this share of its in-links; 0 = never (measured: ER s24 runs 3.95 ms per
+// iteration in row tiles against 1.98 ms split -- the tiles' sweeps do not keep an XCD's waves in
+// one L2-sized region, so nearly every gather misses L2)
+constexpr double kRowsMaxHotCover = 0.0;
 
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {
   int C;
   int64_t Q_pad, S_pad;
-};
-
-// Offsets of the per-class partial-sum arrays (split layout), passed to kernels by value.
-struct PartOff {
-  int64_t o[kMaxClasses + 1];
 };
 
 // Gather positions of every part's {dangling partial, L1 partial} slot pair (the dangling one;
@@ -186,14 +194,9 @@ struct SlotPos {
 struct HotGeom {
   int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;
-  // k_spmv_hot unit -> wave mapping (PR_HOT_ASSIGN A/B): 0 = the XCD's waves interleaved over
-  // its class's units, 1 = one contiguous run of units per wave, 2 = one run per workgroup
-  // with its waves interleaved in it, 3 (the default) = the workgroup's units of mode 0 taken by
-  // its waves from an LDS counter (balanced within the workgroup)
-  int assign;
   __host__ __device__ int slots() const { return P * Kp + 1; }
-  // slot `slots()` is a control word (the workgroup's unit counter of PR_HOT_ASSIGN=3); the
-  // staging windows start 16-byte aligned after it
+  // slot `slots()` is a control word (the workgroup's unit counter, pr_spmv.h hot_class_units);
+  // the staging windows start 16-byte aligned after it
   __host__ __device__ int stage_off() const { return (slots() + 2) & ~1; }
   __host__ __device__ size_t lds_bytes() const {
     return sizeof(double) * ((size_t)stage_off() + (size_t)(kHotThreads / 64) * kStageSlots);

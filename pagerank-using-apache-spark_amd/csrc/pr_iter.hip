@@ -27,6 +27,7 @@
 
 #include "pr_device.h"
 #include "pr_graph.h"
+#include "pr_rows.h"
 #include "pr_spmv.h"
 
 namespace pr {
@@ -152,53 +153,42 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }  // namespace
 
 int prepare_hot_kernel() {
-  for (int v = 0; v < kNumEpiVariants; ++v)
-    for (int c : {8, 16, 32, 64, 128})
-      for (bool walk : {false, true})
-        for (bool narrow : {false, true})
-          PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, v, walk, narrow)),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(v, narrow)));
-  for (const void *k : {reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<0, 0, 0, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<1, 0, 1, false>)})
-    PR_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (int c : {8, 16, 32, 64, 128})
+    for (bool walk : {false, true})
+      for (bool narrow : {false, true}) {
+        if ((walk || narrow) && c > kWave) continue;  // walk and one-wave workgroups: <= 64 classes
+        PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
+      }
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             kHotLdsBytes));
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_rows), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             kRowsLdsBytes));
   return PR_OK;
 }
 
-// The per-row walk of the grouped epilogue (pr_spmv.h k_epilogue_grp WALK): on by default for its
-// variants 0 and 7 at <= 64 classes for the groups that fit one window load (PR_EPI_WALK=1);
-// 0 keeps the class loop everywhere, 2 walks by the step estimate (A/B, k_epi_walk_plan).  Plans
-// which groups walk (k_epi_walk_plan COUNT), places their positions (host prefix over the groups)
-// and writes them.
+// The per-row walk of the grouped epilogue (pr_spmv.h k_epilogue_grp WALK): on by default
+// (PR_BOPT_EPI_WALK) at <= 64 classes for the groups whose runs and slot positions fit one window
+// load.  Plans which groups walk (k_epi_walk_plan COUNT), places their positions (host prefix over
+// the groups) and writes them.
 int plan_epi_walk(pr_graph *g) {
   g->epi_walk = false;
   g->n_walk_groups = 0;
-  int rule = 1;
-  if (const char *e = getenv("PR_EPI_WALK")) rule = std::min(std::max(atoi(e), 0), 2);
-  if (rule == 0 || !g->epi_grp || !epi_walk_variant(g->C, g->epi_var) || g->nblk <= 0) return PR_OK;
-  const int G = kEpiVariants[g->epi_var].G;
-  const int64_t ngrp = (g->nblk + G - 1) / G;
-  using PlanFn = void (*)(int64_t, const void *, const int32_t *, int64_t *, uint16_t *, int);
+  if (!g->opts.epi_walk || g->C > kWave || g->nblk <= 0) return PR_OK;
+  const int64_t ngrp = (g->nblk + kEpiGroup - 1) / kEpiGroup;
+  using PlanFn = void (*)(int64_t, const void *, const int32_t *, int64_t *, uint16_t *);
   PlanFn count = nullptr, write = nullptr;
-  constexpr int G7 = kEpiVariants[7].G, W7 = kEpiVariants[7].W;
-  static_assert(kEpiVariants[0].G == kEpiGroup && kEpiVariants[0].W == kEpiWin, "variant 0 is the default");
-  const bool wide = g->epi_var == 7;
-#define PR_WALK_PLAN(CC)                                                                                   \
-  count = wide ? k_epi_walk_plan<CC, G7, W7, true> : k_epi_walk_plan<CC, kEpiGroup, kEpiWin, true>;        \
-  write = wide ? k_epi_walk_plan<CC, G7, W7, false> : k_epi_walk_plan<CC, kEpiGroup, kEpiWin, false>;
   switch (g->C) {
-    case 8: PR_WALK_PLAN(8) break;
-    case 16: PR_WALK_PLAN(16) break;
-    case 32: PR_WALK_PLAN(32) break;
-    case 64: PR_WALK_PLAN(64) break;
+    case 8: count = k_epi_walk_plan<8, true>, write = k_epi_walk_plan<8, false>; break;
+    case 16: count = k_epi_walk_plan<16, true>, write = k_epi_walk_plan<16, false>; break;
+    case 32: count = k_epi_walk_plan<32, true>, write = k_epi_walk_plan<32, false>; break;
+    case 64: count = k_epi_walk_plan<64, true>, write = k_epi_walk_plan<64, false>; break;
     default: return PR_OK;
   }
-#undef PR_WALK_PLAN
   PR_TRY(g->eoff.alloc(sizeof(int64_t) * (size_t)ngrp));
   const unsigned blocks = grid_for(ngrp, kEpiThreads / kWave, 8192);
   hipLaunchKernelGGL(count, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p, g->cbase.as<int32_t>(),
-                     g->eoff.as<int64_t>(), nullptr, rule);
+                     g->eoff.as<int64_t>(), nullptr);
   PR_HIP(hipGetLastError());
   std::vector<int64_t> off((size_t)ngrp);
   PR_HIP(hipMemcpyAsync(off.data(), g->eoff.p, sizeof(int64_t) * (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
@@ -207,7 +197,7 @@ int plan_epi_walk(pr_graph *g) {
   for (auto &o : off) {
     if (o < 0) continue;
     const int64_t n = o;
-    o = total;  // a multiple of 8 positions: every batch's run of positions is padded to 16 bytes
+    o = total;  // a multiple of 8 positions: every group's run of positions is padded to 16 bytes
     total += n;
     ++g->n_walk_groups;
   }
@@ -215,21 +205,20 @@ int plan_epi_walk(pr_graph *g) {
   PR_HIP(hipMemcpyAsync(g->eoff.p, off.data(), sizeof(int64_t) * (size_t)ngrp, hipMemcpyHostToDevice, g->stream));
   if (total > 0)
     hipLaunchKernelGGL(write, dim3(blocks), dim3(kEpiThreads), 0, g->stream, g->nblk, g->rmask.p,
-                       g->cbase.as<int32_t>(), g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), rule);
+                       g->cbase.as<int32_t>(), g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
   PR_HIP(hipGetLastError());
   PR_HIP(hipStreamSynchronize(g->stream));
   g->epi_walk = true;
   return PR_OK;
 }
 
-int n_hot_phases(const pr_graph *g) { return g->hot_phased ? std::max(1, g->C / kXcds) : 1; }
+int n_hot_phases(const pr_graph *g) { return g->C > 1 ? std::max(1, g->C / kXcds) : 1; }
 
 int set_hot_reserve(pr_graph *g, int per_xcd) {
-  if (per_xcd == 0) {
+  if (per_xcd == 0 || g->C <= 1) {
     g->hot_grid = g->hot_grid_full;
     return PR_OK;
   }
-  if (!g->hot_phased) return fail(PR_ERR_INVALID, "reserving CUs needs the phased k_spmv_hot schedule");
   const int grid = g->hot_grid_full - kXcds * per_xcd;  // still a multiple of kXcds
   if (per_xcd < 0 || grid < kXcds) return fail(PR_ERR_INVALID, "bad CU reserve");
   g->hot_grid = grid;
@@ -237,26 +226,16 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
 }
 
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
-  const size_t lds = g->hot.lds_bytes();
-  // phased: ORDER 1, each unit reduced before the next unit's gathers are issued (-3.7 % at s26,
-  // -6.6 % for a P = 8 part, -3.6 % ER s24: profiles/r02/order_ab/)
-  auto *kern = g->hot_meta ? (g->hot_phased ? &k_spmv_hot<1, 0, 1, false> : &k_spmv_hot<0, 0, 0, false>)
-                           : (g->hot_phased ? &k_spmv_hot<1, 0, 1, true> : &k_spmv_hot<0, 0, 0, true>);
   if (ph1 < 0) ph1 = n_hot_phases(g);
-  hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), lds, g->stream,
+  hipLaunchKernelGGL(k_spmv_hot, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
-                     g->hmeta.as<uint32_t>(), g->cbuf[in].as<double>(),
-                     (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),
+                     g->cbuf[in].as<double>(), (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),
                      g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
 
-void set_exchange_chunking(pr_graph *g) {
-  bool on = false;
-  if (const char *e = getenv("PR_XCHG_CHUNKS")) on = atoi(e) != 0;
-  g->x_chunked = on && g->n_xc > 1;
-}
+void set_exchange_chunking(pr_graph *g) { g->x_chunked = g->opts.xchg_chunks && g->n_xc > 1; }
 
 int join_exchange(pr_graph *g) {
   if (!g->x_pending) return PR_OK;
@@ -311,13 +290,21 @@ int iter_compute(pr_graph *g) {
   }
   // light rows (all rows when C == 1): fused single pass
   if (g->C == 1) PR_TRY(join_exchange(g));
+  if (g->layout == kLayoutRows) {  // row tiles: one launch per pass, the update fused (pr_rows.h)
+    for (int p = 0; p < g->rows_passes; ++p)
+      hipLaunchKernelGGL(k_spmv_rows, dim3((unsigned)g->rows_grid), dim3(kRowsThreads), kRowsLdsBytes, s, p,
+                         g->n_tiles, g->tile_u.as<int64_t>(), g->rcodes.as<uint32_t>(), g->rrows.as<uint16_t>(),
+                         g->cbuf[in].as<double>(), (uint32_t)(sizeof(double) * g->gsize),
+                         g->cbuf[out].as<double>() + own, g->r.as<double>(), g->rowinfo.as<uint32_t>(), g->n_rows,
+                         g->slots, (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>());
+  }
   if (g->n_units > 0)
     hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
                        g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
                        g->rowinfo.as<uint32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
-                       g->slots, g->S_pad, (double)g->V, g->teleport, g->damping, 0xFFFFFFFFu);
-  int64_t n_parts = g->n_units;
+                       g->slots, g->S_pad, (double)g->V, g->teleport, g->damping);
+  int64_t n_parts = g->layout == kLayoutRows ? g->ep_blocks : g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
     const int nph = n_hot_phases(g);
     if (g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1) {
@@ -335,24 +322,12 @@ int iter_compute(pr_graph *g) {
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
-    if (g->epi_grp) {
-      const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_var, g->epi_walk, g->epi_narrow);
-      const size_t lds = epi_grp_lds(g->epi_var, g->epi_narrow);
-      hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_var, g->epi_narrow)), lds, s, g->nblk, g->partial.as<double>(),
-                         g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
-                         g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
-                         (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
-                         g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
-    } else {
-    auto *epi = g->epi_abs ? (g->C == 32 ? k_epilogue<32, true> : (g->C == 16 ? k_epilogue<16, true> : k_epilogue<8, true>))
-                           : (g->C == 32 ? k_epilogue<32> : (g->C == 16 ? k_epilogue<16> : k_epilogue<8>));
-    hipLaunchKernelGGL(epi, dim3(g->ep_blocks),
-                       dim3(kThreads), 0, s, g->nblk, g->part_off, g->partial.as<double>(),
-                       g->rmask.as<uint32_t>(), g->cbase.as<int32_t>(),
-                       g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
-                       g->cbuf[in].as<double>(), g->slots, (double)g->V, g->teleport, g->damping,
-                       g->unit_part.as<double2>() + g->n_units);
-    }
+    const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
+    hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
+                       g->nblk, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                       g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
+                       (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
+                       g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
     n_parts += g->ep_blocks;
   }
   PR_HIP(hipGetLastError());

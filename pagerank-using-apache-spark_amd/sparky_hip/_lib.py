@@ -15,6 +15,8 @@ BUILD_DIR = os.path.join(os.path.dirname(_PKG_DIR), "build")
 # PR_LIB_PATH: another build of the same library (A/B of two kernel versions on one box)
 LIB_PATH = os.environ.get("PR_LIB_PATH") or os.path.join(BUILD_DIR, "libpagerank_hip.so")
 
+ABI_VERSION = 2  # include/pagerank_hip.h PR_ABI_VERSION this binding was written against
+
 PR_OK = 0
 PR_ERR_INVALID = -1
 PR_ERR_HIP = -2
@@ -29,13 +31,17 @@ PR_INPUT_DEVICE = 2
 PR_NO_CANONICAL = 4
 PR_LAYOUT_FUSED = 8
 PR_LAYOUT_SPLIT = 16
+PR_LAYOUT_ROWS = 32
 
 PR_VF_KEY, PR_VF_SINK, PR_VF_NOLINK, PR_VF_INDEG0 = 1, 2, 4, 8
 
 INFO_NAMES = ["n_vertices", "n_edges", "n_sink", "n_nolink", "n_indeg0", "max_indeg", "local_rows",
               "local_edges", "part", "n_parts", "n_units", "n_long_rows", "device_bytes", "classes",
               "xchg_send", "xchg_recv", "partial_slots", "hot_slots", "epilogue", "gather_est",
-              "walk_groups"]
+              "walk_groups", "layout", "hot_cover_ppm", "launches"]
+# build options of pr_graph_create_ex (PR_BOPT_*), by the keyword PageRankGraph(options=...) takes
+BUILD_OPTIONS = {"classes": 1, "hot_slots": 2, "exchange_allgather": 3, "xchg_chunks": 4, "hot_reserve": 5,
+                 "epi_walk": 6, "epi_narrow": 7}
 STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "iter_ms_mean",
               "build_ms", "exchange_ms_mean"]
 PR_CB_RANKS = 1
@@ -46,6 +52,7 @@ PR_COMM_ID_BYTES = 128
 # Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "pr_abi_version", "pr_last_error", "pr_device_count", "pr_graph_create", "pr_graph_create_part",
+    "pr_graph_create_ex",
     "pr_graph_info", "pr_graph_export_csr", "pr_run", "pr_reset", "pr_step", "pr_sync",
     "pr_get_ranks", "pr_set_timing", "pr_set_option", "pr_get_stats", "pr_comm_unique_id", "pr_graph_attach_comm",
     "pr_graph_destroy", "pr_gen_rmat", "pr_gen_er", "pr_gen_chunglu", "pr_intern_device", "pr_group_reset",
@@ -94,6 +101,7 @@ def load() -> ctypes.CDLL:
         "pr_device_count": ([P], ctypes.c_int),
         "pr_graph_create": ([i32, i32, i64, P, P, u32, P], ctypes.c_int),
         "pr_graph_create_part": ([i32, i32, i32, i32, i64, P, P, u32, P], ctypes.c_int),
+        "pr_graph_create_ex": ([i32, i32, i32, i32, i64, P, P, u32, P, i32, P], ctypes.c_int),
         "pr_graph_info": ([P, P, i32], ctypes.c_int),
         "pr_graph_export_csr": ([P, P, P, P, P], ctypes.c_int),
         "pr_run": ([P, i32, dbl, dbl, P, P, ITER_CB, u32, P], ctypes.c_int),
@@ -119,6 +127,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    v = L.pr_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI version {v}; this binding needs {ABI_VERSION} (rebuild the library)")
     _lib = L
     return L
 

@@ -62,11 +62,14 @@ class PageRankGraph:
 
     def __init__(self, n_vertices: int, src, dst, *, device: int = 0, dangling: str = "local",
                  part: int = 0, n_parts: int = 1, keep_canonical: bool = True,
-                 device_input: bool = False, n_edges: Optional[int] = None, layout: str = "auto"):
+                 device_input: bool = False, n_edges: Optional[int] = None, layout: str = "auto",
+                 options: Optional[dict] = None):
         """src/dst: int32 host arrays (numpy) of raw interned edges, dst == -1 for a record
         without links; or, with device_input=True, integer device addresses (e.g. from
-        torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (column classes once the
-        contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h)."""
+        torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (the size and hot-set policy),
+        'fused', 'split' (column classes) or 'rows' (row tiles) (pr_graph.h).  options: build
+        options of pr_graph_create_ex by name (_lib.BUILD_OPTIONS: classes, hot_slots,
+        exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow)."""
         L = _lib.load()
         flags = 0
         if dangling == "none":
@@ -79,8 +82,10 @@ class PageRankGraph:
             flags |= _lib.PR_LAYOUT_FUSED
         elif layout == "split":
             flags |= _lib.PR_LAYOUT_SPLIT
+        elif layout == "rows":
+            flags |= _lib.PR_LAYOUT_ROWS
         elif layout != "auto":
-            raise ValueError("layout must be 'auto', 'fused' or 'split'")
+            raise ValueError("layout must be 'auto', 'fused', 'split' or 'rows'")
         if device_input:
             flags |= _lib.PR_INPUT_DEVICE
             if n_edges is None:
@@ -95,7 +100,15 @@ class PageRankGraph:
             ps, pd = _ptr(src), _ptr(dst)
             ne = int(src.shape[0])
         self._h = ctypes.c_void_p()
-        if n_parts == 1 and part == 0:
+        opts = options or {}
+        unknown = set(opts) - set(_lib.BUILD_OPTIONS)
+        if unknown:
+            raise ValueError(f"unknown build options {sorted(unknown)}")
+        kv = np.array([x for k, v in opts.items() for x in (_lib.BUILD_OPTIONS[k], int(v))], np.int64)
+        if opts:
+            rc = L.pr_graph_create_ex(device, part, n_parts, int(n_vertices), ne, ps, pd, flags, _ptr(kv), len(opts),
+                                      ctypes.byref(self._h))
+        elif n_parts == 1 and part == 0:
             rc = L.pr_graph_create(device, int(n_vertices), ne, ps, pd, flags, ctypes.byref(self._h))
         else:
             rc = L.pr_graph_create_part(device, part, n_parts, int(n_vertices), ne, ps, pd, flags,

@@ -38,12 +38,13 @@ def assert_csr_equal(g, csr):
     assert np.array_equal(ex.vflags, csr.vflags)
 
 
-def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, layout="auto"):
+def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, layout="auto", options=None):
     csr = oracle_c.build_csr(V, src, dst)
     ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
-    with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout) as g:
+    with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout, options=options) as g:
         if layout != "auto":
-            assert g.info()["classes"] in ((1,) if layout == "fused" else (8, 16, 32, 64, 128))
+            assert g.info()["layout"] == {"fused": 0, "split": 1, "rows": 2}[layout]
+            assert g.info()["classes"] in ((8, 16, 32, 64, 128) if layout == "split" else (1,))
         assert_csr_equal(g, csr)
         hist = []
         ranks, stats = g.run(iters, init_ranks=init, want_ranks_in_callback=True,
@@ -97,7 +98,7 @@ def random_edges(rng, V, E, p_nolink=0.05, hub_frac=0.0):
     return src.astype(np.int32), dst.astype(np.int32)
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 @pytest.mark.parametrize("V,E,seed", [(1, 1, 0), (17, 60, 1), (1000, 9000, 2), (50000, 800000, 3)])
 def test_random_graphs(hip, oracle_c, V, E, seed, layout):
     rng = np.random.default_rng(seed)
@@ -109,7 +110,7 @@ def test_random_graphs(hip, oracle_c, V, E, seed, layout):
         assert abs(stats[it].l1_delta - ref["l1"][it]) <= 1e-9 * max(ref["l1"][it], 1.0)
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 def test_long_rows_and_unit_boundaries(hip, oracle_c, layout):
     """Hubs split into many 2048-in-link pieces, rows of exactly 2048 / 2049 in-links, and a
     run of > 1024 short rows (the per-unit row cap)."""
@@ -128,14 +129,16 @@ def test_long_rows_and_unit_boundaries(hip, oracle_c, layout):
     assert indeg[1] == 2048 and indeg[2] == 2049 and indeg[4] == 2047
     if layout == "fused":
         assert info["n_long_rows"] == int(np.sum(indeg > 2048)) == 4  # 70000, 2049, 4096, 6144
-    else:  # long (row, class) segments: the 70000-in-link hub splits into 8 long segments
+    elif layout == "split":  # long (row, class) segments: the 70000-in-link hub splits into 8 long segments
         assert info["n_long_rows"] >= 8
+    else:  # row tiles: a hub's in-links are cut at unit ends, every piece added to its LDS row sum
+        assert info["layout"] == 2 and info["n_long_rows"] == 0 and info["epilogue"] == 4
     assert info["max_indeg"] == 70000
     for it in range(8):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 def test_heavy_hub_and_many_indeg0(hip, oracle_c, layout):
     rng = np.random.default_rng(4)
     src, dst = random_edges(rng, 20000, 300000, p_nolink=0.2, hub_frac=0.3)
@@ -144,7 +147,7 @@ def test_heavy_hub_and_many_indeg0(hip, oracle_c, layout):
     assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 def test_dangling_none(hip, oracle_c, layout):
     rng = np.random.default_rng(5)
     src, dst = random_edges(rng, 3000, 20000)
@@ -164,7 +167,7 @@ def test_resume_from_saved_ranks(hip, oracle_c):
     assert max_rel(r3_2, r5) <= 1e-13
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 def test_deterministic_bitwise(hip, layout):
     rng = np.random.default_rng(7)
     src, dst = random_edges(rng, 40000, 600000, hub_frac=0.05)
@@ -262,21 +265,20 @@ def test_device_generator_and_interning(hip, oracle_c, gen, scale, ef, layout):
 
 
 @pytest.mark.parametrize("slots", [0, 37, 1000])
-def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
-    """A hot set smaller than the class regions (PR_HOT_SLOTS, read at build time): most entries
-    take k_spmv_hot's gather-space loads instead of the LDS -- the path every large graph uses --
-    with hub segments split into pieces, empty (row, class) pairs and several parts."""
-    monkeypatch.setenv("PR_HOT_SLOTS", str(slots))
-    monkeypatch.setenv("PR_CLASSES", "16")  # 16 classes: segments long enough to need pieces
+def test_split_gather_space_path(hip, oracle_c, slots):
+    """A hot set smaller than the class regions (PR_BOPT_HOT_SLOTS): most entries take
+    k_spmv_hot's gather-space loads instead of the LDS -- the path every large graph uses -- with
+    hub segments split into pieces, empty (row, class) pairs and several parts."""
+    opts = {"hot_slots": slots, "classes": 16}  # 16 classes: segments long enough to need pieces
     rng = np.random.default_rng(40 + slots)
     V = 30000
     src, dst = random_edges(rng, V, 400000, hub_frac=0.03)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10, layout="split")
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 10, layout="split", options=opts)
     assert info["n_long_rows"] > 0
     for it in range(10):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
         assert abs(stats[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
-    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout="split")
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout="split", options=opts)
              for p in range(3)]
     try:
         r = hip.PartGroup(parts).run(10)
@@ -286,35 +288,21 @@ def test_split_gather_space_path(hip, oracle_c, slots, monkeypatch):
             p.close()
 
 
-@pytest.mark.parametrize("classes,phased,epi_abs,epi_grp", [(8, "0", "1", "1"), (16, "0", "0", "1"), (16, "1", "1", "0"),
-                                                             (16, "1", "1", "1"), (32, "0", "0", "1"),
-                                                             (32, "1", "1", "0"), (32, "1", "1", "1"),
-                                                             (32, "1", "1", "v1"), (32, "1", "1", "v2"),
-                                                             (32, "1", "1", "v4"), (64, "0", "1", "1"),
-                                                             (64, "1", "1", "1"), (64, "1", "1", "v2"),
-                                                             (64, "1", "0", "1"), (128, "0", "1", "1"),
-                                                             (128, "1", "1", "1"), (128, "1", "0", "v2"),
-                                                             (64, "1", "1", "v6")])
-def test_split_class_schedules(hip, oracle_c, classes, phased, epi_abs, epi_grp, monkeypatch):
-    """Every class count with both k_spmv_hot schedules (an XCD's classes concurrently, or one
-    after another with the hot set restaged per class) and the three epilogues: grouped (class
-    runs of 8 blocks staged in LDS; here ~10 segments per row, so a group's runs take several
-    window loads), one load per class and block over all partials, or one buffer per class (the
-    > 2^29-slot path, which also turns the grouped one off); the grouped one in several (blocks
-    per group, LDS window) variants.  (64, PR_EPI_ABS=0): the grouped epilogue without the
-    < 2^29-slot byte-offset path, as a graph with more than 2^29 partial slots builds it.  128
-    classes: four mask words per row.  Default policy: up to 64 classes, phased, grouped."""
-    monkeypatch.setenv("PR_CLASSES", str(classes))
-    monkeypatch.setenv("PR_HOT_PHASED", phased)
-    monkeypatch.setenv("PR_EPI_ABS", epi_abs)
-    monkeypatch.setenv("PR_EPI_GRP", "0" if epi_grp == "0" else "1")
-    monkeypatch.setenv("PR_EPI_VAR", epi_grp[1:] if epi_grp.startswith("v") else "0")
-    monkeypatch.setenv("PR_HOT_SLOTS", "300")
+@pytest.mark.parametrize("classes,narrow", [(8, -1), (16, -1), (32, 0), (32, 1), (64, 0), (64, 1), (128, -1),
+                                            (128, 1)])
+def test_split_class_schedules(hip, oracle_c, classes, narrow):
+    """Every class count through the phased k_spmv_hot (the hot set restaged per class) and the
+    grouped epilogue (class runs of 8 blocks staged in LDS; here ~10 segments per row, so a group's
+    runs take several window loads) with four-wave and one-wave workgroups.  128 classes: four mask
+    words per row, and one-wave workgroups are refused (PR_BOPT_EPI_NARROW=1 falls back to four
+    waves: ADVICE r2, the kernel at 128 classes strides its groups by four waves).  Default policy:
+    up to 64 classes."""
+    opts = {"classes": classes, "hot_slots": 300, "epi_narrow": narrow}
     rng = np.random.default_rng(90 + classes)
     V = 50000
     src, dst = random_edges(rng, V, 600000, hub_frac=0.03)
-    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 6, layout="split")
-    assert info["classes"] == classes
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 6, layout="split", options=opts)
+    assert info["classes"] == classes and info["layout"] == 1
     for it in range(6):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
@@ -342,7 +330,7 @@ def test_rmat_s20_split_default_hot_set(hip, oracle_c):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 def test_chunglu_generator_small(hip, oracle_c, layout):
     """The Chung-Lu generator (LJ / Twitter shapes) on a small instance with sink-only ranks and
     link-less records: raw labels in range, the link-less records present, interning equal to the
@@ -397,46 +385,45 @@ def test_lj_shaped_full_size(hip, oracle_c):
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
 
 
-@pytest.mark.parametrize("layout", ["fused", "split"])
-def test_compacted_gather_space_is_bitwise_whole_slices(hip, layout, monkeypatch):
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+def test_compacted_gather_space_is_bitwise_whole_slices(hip, layout):
     """The compacted gather space (own slice + received runs) keeps every row's summation order,
-    so its ranks equal the whole-slice all-gather layout's bit for bit."""
+    so its ranks equal the whole-slice all-gather layout's bit for bit.  (Row tiles sweep their
+    in-links by region of the gather space, so there the order -- not the sums -- follows the
+    space: equal to rounding.)"""
     rng = np.random.default_rng(77)
     V = 30000
     src, dst = random_edges(rng, V, 300000, hub_frac=0.05)
     out = {}
     for xmode in ("sparse", "allgather"):
-        if xmode == "allgather":
-            monkeypatch.setenv("PR_EXCHANGE", "allgather")
-        else:
-            monkeypatch.delenv("PR_EXCHANGE", raising=False)
-        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout=layout)
+        opts = {"exchange_allgather": int(xmode == "allgather")}
+        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=3, keep_canonical=False, layout=layout, options=opts)
                  for p in range(3)]
         try:
             out[xmode] = hip.PartGroup(parts).run(8)
         finally:
             for p in parts:
                 p.close()
-    assert np.array_equal(out["sparse"], out["allgather"])
+    if layout == "rows":
+        assert max_rel(out["sparse"], out["allgather"]) <= 1e-13
+    else:
+        assert np.array_equal(out["sparse"], out["allgather"])
 
 
 @pytest.mark.parametrize("xmode", ["sparse", "allgather"])
-@pytest.mark.parametrize("layout", ["fused", "split"])
+@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
-def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode, monkeypatch):
+def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode):
     """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
-    exchange moves the packed per-peer runs (or whole slices, PR_EXCHANGE=allgather) by device
+    exchange moves the packed per-peer runs (or whole slices, PR_BOPT_EXCHANGE = 1) by device
     copies (RCCL send/recv carries the same runs across processes)."""
-    if xmode == "allgather":
-        monkeypatch.setenv("PR_EXCHANGE", "allgather")
-    else:
-        monkeypatch.delenv("PR_EXCHANGE", raising=False)
+    opts = {"exchange_allgather": int(xmode == "allgather")}
     rng = np.random.default_rng(30 + P)
     V = 40000
     src, dst = random_edges(rng, V, 500000, hub_frac=0.05)
     csr = oracle_c.build_csr(V, src, dst)
     ref = oracle_c.run(csr, 10)
-    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout=layout)
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout=layout, options=opts)
              for p in range(P)]
     try:
         infos = [p.info() for p in parts]
@@ -469,15 +456,13 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode, monkeyp
 
 
 @pytest.mark.parametrize("P", [2, 8])
-def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
+def test_overlapped_exchange_chunks(hip, oracle_c, P):
     """The overlapped exchange (pr_exchange.hip): with 64 classes the phased k_spmv_hot runs 8
     phases and every peer's run travels in 8 chunks, chunk c = the positions of classes [8c, 8c+8);
     the next iteration's phase c waits only for chunk c.  Against the oracle, and bitwise equal to
-    the same parts exchanging whole runs before the next iteration starts (PR_XCHG_CHUNKS=0): the
-    chunking moves the same values, only earlier.  PR_XCHG_CHUNKS=1 forces the chunking, which a
-    group whose parts share one GPU leaves off by default."""
-    monkeypatch.setenv("PR_CLASSES", "64")
-    monkeypatch.setenv("PR_HOT_SLOTS", "600")
+    the same parts exchanging whole runs before the next iteration starts (PR_BOPT_XCHG_CHUNKS=0):
+    the chunking moves the same values, only earlier.  PR_BOPT_XCHG_CHUNKS=1 forces the chunking,
+    which a group whose parts share one GPU leaves off by default."""
     rng = np.random.default_rng(60 + P)
     V = 60000
     src, dst = random_edges(rng, V, 700000, hub_frac=0.02)
@@ -485,9 +470,9 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
     ref = oracle_c.run(csr, 9)
     out = {}
     for chunks in ("on", "off", "opt"):
-        monkeypatch.setenv("PR_XCHG_CHUNKS", "1" if chunks == "on" else "0")
-        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split")
-                 for p in range(P)]
+        opts = {"classes": 64, "hot_slots": 600, "xchg_chunks": int(chunks == "on")}
+        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split",
+                                   options=opts) for p in range(P)]
         try:
             assert all(p.info()["classes"] == 64 for p in parts)
             if chunks == "opt":  # also with one CU per XCD left free (PR_OPT_HOT_RESERVE)
@@ -507,80 +492,34 @@ def test_overlapped_exchange_chunks(hip, oracle_c, P, monkeypatch):
     assert max_rel(out["on"], ref["ranks"]) <= RANK_TOL
 
 
-def test_lane_metadata_in_kernel_equals_precomputed(hip, oracle_c, monkeypatch):
-    """k_spmv_hot derives each lane's segment metadata from the end marks in its codes
-    (pr_spmv.h derive_meta); PR_HOT_META=1 reads the same words precomputed at build (hmeta).
-    Same sums, bit for bit, and both equal the oracle."""
-    monkeypatch.setenv("PR_CLASSES", "16")
-    monkeypatch.setenv("PR_HOT_SLOTS", "500")
-    rng = np.random.default_rng(123)
-    V = 40000
-    src, dst = random_edges(rng, V, 500000, hub_frac=0.03)
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("PR_HOT_META", mode)
-        with hip.PageRankGraph(V, src, dst, layout="split", keep_canonical=False) as g:
-            out[mode], _ = g.run(8)
-    assert np.array_equal(out["0"], out["1"])
-    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
-    assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
-
-
-def test_unit_assignment_modes_bitwise(hip, oracle_c, monkeypatch):
-    """k_spmv_hot's unit -> wave mappings (PR_HOT_ASSIGN 0: interleaved over the XCD, 1: a run per
-    wave, 2: a run per workgroup, 3: the workgroup's waves take units from an LDS counter) and a
-    reserved CU per XCD (PR_HOT_RESERVE=1) only change which wave reduces a unit: bitwise equal
-    ranks, and the oracle's."""
-    monkeypatch.setenv("PR_CLASSES", "32")
-    monkeypatch.setenv("PR_HOT_SLOTS", "700")
+def test_hot_reserve_bitwise(hip, oracle_c):
+    """k_spmv_hot with 0 / 1 / 2 CUs per XCD left free (PR_BOPT_HOT_RESERVE, or pr_set_option
+    later): only which wave reduces a unit changes, so the ranks are bitwise equal, and the
+    oracle's."""
     rng = np.random.default_rng(77)
     V = 50000
     src, dst = random_edges(rng, V, 600000, hub_frac=0.02)
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 7)
     out = {}
-    for mode in ("0", "1", "2", "3", "3r"):
-        monkeypatch.setenv("PR_HOT_ASSIGN", mode[0])
-        monkeypatch.setenv("PR_HOT_RESERVE", "1" if mode.endswith("r") else "0")
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+    for mode in ("0", "1", "2", "opt1"):
+        opts = {"classes": 32, "hot_slots": 700, "hot_reserve": 0 if mode.startswith("opt") else int(mode)}
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split", options=opts) as g:
             assert g.info()["classes"] == 32
+            if mode == "opt1":
+                g.set_hot_reserve(1)
             out[mode], _ = g.run(7)
     for mode in out:
         assert np.array_equal(out[mode], out["0"]), mode
     assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
 
 
-def test_epilogue_staging_modes_bitwise(hip, oracle_c, monkeypatch):
-    """k_epilogue_grp stages a group's class runs by prefix batches (one ballot per window load)
-    or, PR_EPI_VAR=6, by the round-1 per-class fill loop: the same runs at the same window
-    positions, so the row sums -- and the ranks -- are bitwise equal."""
-    monkeypatch.setenv("PR_CLASSES", "64")
-    monkeypatch.setenv("PR_HOT_SLOTS", "400")
-    monkeypatch.setenv("PR_EPI_NARROW", "0")  # variant 6 has four-wave workgroups only
-    rng = np.random.default_rng(31)
-    V = 70000
-    src, dst = random_edges(rng, V, 900000, hub_frac=0.03)
-    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 6)
-    out = {}
-    for var in ("0", "6"):
-        monkeypatch.setenv("PR_EPI_VAR", var)
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
-            assert g.info()["classes"] == 64 and g.info()["epilogue"] == 3
-            out[var], _ = g.run(6)
-    assert np.array_equal(out["0"], out["6"])
-    assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
-
-
-@pytest.mark.parametrize("classes,var", [("64", "0"), ("32", "0"), ("16", "7"), ("64", "7")])
-def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
-    """k_epilogue_grp walks the rows of sparse groups over their own slots (PR_EPI_WALK=1, the
-    default: groups that fit one window load; 2: by step estimate, multi-batch) instead of looping
-    over every class: the same slots added in the same class order, so the ranks are bitwise
-    those of the class loop (PR_EPI_WALK=0), for dense groups and sparse tails alike, and within
-    the bar of the oracle (Sparky.java:229-233)."""
-    monkeypatch.setenv("PR_CLASSES", classes)
-    monkeypatch.setenv("PR_HOT_SLOTS", "400")
-    monkeypatch.setenv("PR_EPI_VAR", var)
-    monkeypatch.setenv("PR_EPI_NARROW", "0")  # the same workgroup shape (block partial tree) in every run
+@pytest.mark.parametrize("classes", ["64", "32", "16"])
+def test_epilogue_row_walk_bitwise(hip, oracle_c, classes):
+    """k_epilogue_grp walks the rows of sparse groups over their own slots (PR_BOPT_EPI_WALK=1,
+    the default: groups that fit one window load) instead of looping over every class: the same
+    slots added in the same class order, so the ranks are bitwise those of the class loop
+    (PR_BOPT_EPI_WALK=0), for dense groups and sparse tails alike, and within the bar of the oracle
+    (Sparky.java:229-233)."""
     rng = np.random.default_rng(47)
     C = int(classes)
     V = max(90000, 1024 * C)
@@ -594,9 +533,10 @@ def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
     src, dst = np.concatenate([src, dense_src]), np.concatenate([dst, dense_dst])
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 6)
     out = {}
-    for walk in ("1", "2", "0"):  # one-window groups (default), by step estimate, never
-        monkeypatch.setenv("PR_EPI_WALK", walk)
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+    for walk in ("1", "0"):  # one-window groups (default), never
+        # the same workgroup shape (block partial tree) in every run
+        opts = {"classes": int(classes), "hot_slots": 400, "epi_narrow": 0, "epi_walk": int(walk)}
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split", options=opts) as g:
             info = g.info()
             assert info["classes"] == int(classes) and info["epilogue"] == 3
             ngrp = -(-info["local_rows"] // 512)
@@ -605,23 +545,22 @@ def test_epilogue_row_walk_bitwise(hip, oracle_c, monkeypatch, classes, var):
             else:
                 assert info["walk_groups"] == 0
             out[walk], _ = g.run(6)
-    assert np.array_equal(out["1"], out["0"]) and np.array_equal(out["2"], out["0"])
+    assert np.array_equal(out["1"], out["0"])
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
 
 
-def test_epilogue_narrow_workgroups(hip, oracle_c, monkeypatch):
-    """One-wave epilogue workgroups (PR_EPI_NARROW=1; picked by default when many groups walk)
+def test_epilogue_narrow_workgroups(hip, oracle_c):
+    """One-wave epilogue workgroups (PR_BOPT_EPI_NARROW=1; picked by default when many groups walk)
     against four-wave ones: the same row sums, the {dangling, L1} block partials in another fixed
     tree, so the ranks agree to rounding, repeat bitwise, and meet the oracle bar."""
-    monkeypatch.setenv("PR_CLASSES", "32")
     rng = np.random.default_rng(71)
     V = 80000
     src, dst = random_edges(rng, V, 160000, hub_frac=0.02)
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
     out = {}
     for narrow in ("1", "0"):
-        monkeypatch.setenv("PR_EPI_NARROW", narrow)
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split") as g:
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split",
+                               options={"classes": 32, "epi_narrow": int(narrow)}) as g:
             assert g.info()["epilogue"] == 3 and g.info()["walk_groups"] > 0
             out[narrow], _ = g.run(8)
             again, _ = g.run(8)
@@ -629,3 +568,52 @@ def test_epilogue_narrow_workgroups(hip, oracle_c, monkeypatch):
     assert max_rel(out["1"], out["0"]) <= 1e-13
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
 
+
+
+def test_rows_layout_tiles(hip, oracle_c):
+    """The row-block layout (pr_rows.h k_spmv_rows, PR_LAYOUT_ROWS) on a uniform graph: the sums
+    have a fixed order (bitwise repeatable), no partial slots exist, and every iteration meets the
+    oracle bar -- with several passes (more tiles than waves) and tiles whose streams cross many
+    regions."""
+    rng = np.random.default_rng(2024)
+    V = 1_200_000  # > 4 MiB of contributions: beyond the fused layout; 1172 tiles
+    E = 16 * V
+    src = rng.integers(0, V, E).astype(np.int32)
+    dst = rng.integers(0, V, E).astype(np.int32)
+    seen = np.zeros(V, bool)
+    seen[src] = True
+    seen[dst] = True
+    miss = np.nonzero(~seen)[0].astype(np.int32)
+    src, dst = np.concatenate([src, miss]), np.concatenate([dst, np.full(miss.shape, -1, np.int32)])
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 6, keep_history=True)
+    hist = []
+    with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="rows") as g:
+        info = g.info()
+        assert info["layout"] == 2 and info["epilogue"] == 4 and info["partial_slots"] == 0, info
+        r, st = g.run(6, want_ranks_in_callback=True, callback=lambda it, rr, ss: hist.append(rr))
+        again, _ = g.run(6)
+    assert np.array_equal(r, again)
+    for it in range(6):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+        assert abs(st[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
+        assert abs(st[it].l1_delta - ref["l1"][it]) <= RANK_TOL * max(ref["l1"][it], 1.0)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_rows_layout_partitioned(hip, oracle_c, P):
+    """Row tiles of a row partition: each part's sweep reads its compacted gather space (own slice
+    + received runs), with the exchange after every pass."""
+    rng = np.random.default_rng(55 + P)
+    V = 40000
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.02)
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="rows")
+             for p in range(P)]
+    try:
+        assert all(p.info()["layout"] == 2 for p in parts)
+        r = hip.PartGroup(parts).run(8)
+    finally:
+        for p in parts:
+            p.close()
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL

@@ -45,6 +45,54 @@ def test_ffm_binding_matches_the_c_abi():
         assert re.search(rf"\b{name} = {v}\b", src), name
 
 
+def java_sources():
+    d = os.path.join(JAVA, "src", "sparky", "hip")
+    return {f[:-5]: open(os.path.join(d, f)).read() for f in os.listdir(d) if f.endswith(".java")}
+
+
+def jni_closure(srcs):
+    """Classes of this package the JNI driver reaches (through any reference in their text)."""
+    seen, todo = set(), ["SparkyJni", "PageRankJni"]
+    while todo:
+        c = todo.pop()
+        if c in seen:
+            continue
+        seen.add(c)
+        body = re.sub(r"//[^\n]*|/\*.*?\*/", "", srcs[c], flags=re.S)  # comments may name anything
+        todo += [o for o in srcs if o != c and re.search(rf"\b{o}\b", body)]
+    return seen
+
+
+def test_jni_path_has_no_ffm_and_java8_syntax():
+    """the JNI path must compile on JDK 8..21 -- no java.lang.foreign in any class it
+    reaches, directly or through a referenced class, and no post-Java-8 syntax or API."""
+    srcs = java_sources()
+    closure = jni_closure(srcs)
+    assert closure == {"SparkyJni", "PageRankJni", "SparkyHost", "IterationListener"}, closure
+    java9plus = [r"\.strip\(\)", r"\bPath\.of\(", r"\bList\.of\(", r"\bMap\.of\(", r"\bSet\.of\(",
+                 r"\bvar\s+\w+\s*=", r"case [^:\n]*->", r"\.isBlank\(\)", r'\"\"\"', r"\brecord\s+\w+\s*\(",
+                 r"Files\.readString", r"\.repeat\(", r"\btry\s*\(\s*\w+\s*\)"]
+    for c in closure:
+        body = re.sub(r"//[^\n]*|/\*.*?\*/", "", srcs[c], flags=re.S)
+        assert "java.lang.foreign" not in body, c
+        for pat in java9plus:
+            assert not re.search(pat, body), (c, pat)
+    # the FFM classes are outside the closure and are the only ones importing java.lang.foreign
+    code = {c: re.sub(r"//[^\n]*|/\*.*?\*/", "", b, flags=re.S) for c, b in srcs.items()}
+    assert [c for c in code if "java.lang.foreign" in code[c]] == ["PageRankHip"]
+
+
+def test_bindings_check_the_abi_version():
+    hdr = open(os.path.join(ROOT, "include", "pagerank_hip.h")).read()
+    v = int(re.search(r"#define PR_ABI_VERSION (\d+)", hdr).group(1))
+    srcs = java_sources()
+    for c in ("PageRankJni", "PageRankHip"):
+        assert re.search(rf"ABI_VERSION = {v};", srcs[c]), c
+    glue = open(os.path.join(JAVA, "jni", "pagerank_jni.c")).read()
+    for m in re.findall(r"public static native \w+(?:\[\])? (\w+)\(", srcs["PageRankJni"]):
+        assert f"Java_sparky_hip_PageRankJni_{m}(" in glue, m
+
+
 STUB_JNI = r"""
 typedef int jint; typedef long long jlong; typedef unsigned char jboolean; typedef double jdouble; typedef int jsize;
 typedef void *jobject; typedef jobject jclass, jintArray, jdoubleArray, jarray, jthrowable; typedef struct _jm *jmethodID;
@@ -84,5 +132,9 @@ def test_javac_when_available(tmp_path):
     if not javac:
         pytest.skip("no JDK in this image: the Java host is compiled only where javac exists")
     srcs = [os.path.join(JAVA, "src", "sparky", "hip", f) for f in os.listdir(os.path.join(JAVA, "src", "sparky", "hip"))]
+    d = os.path.join(JAVA, "src", "sparky", "hip")
+    jni = [os.path.join(d, f + ".java") for f in ("IterationListener", "PageRankJni", "SparkyHost", "SparkyJni")]
+    res = subprocess.run([javac, "--release", "8", "-d", str(tmp_path / "jni")] + jni, capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr
     res = subprocess.run([javac, "--release", "22", "-d", str(tmp_path)] + srcs, capture_output=True, text=True)
     assert res.returncode == 0, res.stderr

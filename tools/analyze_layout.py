@@ -12,6 +12,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
@@ -28,7 +29,13 @@ def main():
     ap.add_argument("--classes", type=int, default=64)
     ap.add_argument("--hot", type=int, default=18430)
     a = ap.parse_args()
+    t0 = time.perf_counter()
+
+    def note(msg):
+        print(f"[{time.perf_counter() - t0:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
     wl = generate(a.graph, scale=a.scale)
+    note("generated")
     V = wl.n_vertices
     s, d = wl.src.long(), wl.dst.long()
     del wl
@@ -39,6 +46,7 @@ def main():
     dst = key >> 32
     del key
     E = int(src.numel())
+    note(f"deduped: E'={E}")
     deg = torch.bincount(src, minlength=V)
     order = torch.argsort(-deg * (1 << 32) + torch.arange(V, device=deg.device), stable=True)
     rank = torch.empty_like(order)
@@ -48,6 +56,7 @@ def main():
     hot = (rank[src] // C) < a.hot
     out = {"graph": a.graph, "scale": a.scale, "V": V, "E": E, "classes": C, "hot_slots": a.hot,
            "hot_entries": int(hot.sum())}
+    note("classes")
     # segments (row, class): dst-major keys; count entries and hot entries per segment
     seg = dst * C + cls
     seg_sorted, perm = torch.sort(seg)
@@ -57,6 +66,7 @@ def main():
     nseg = int(uniq.numel())
     hcnt = torch.zeros(nseg, dtype=torch.int64, device=cnt.device).index_add_(0, inv, hot_s)
     ccnt = cnt - hcnt
+    note(f"segments: {nseg}")
     out["segments"] = nseg
     out["segments_singleton"] = int((cnt == 1).sum())
     out["segments_hot_only"] = int((ccnt == 0).sum())

@@ -13,10 +13,10 @@
 #                     never combined with trace domains) + tools/pmc_summary.py
 #   counters:<c1,c2>  one rocprofv3 --pmc pass with these counters on bench.py --no-cpu-baseline
 #                     --steps 5 (respect the per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
-#   diag:<args>       python tools/diag_spmv.py <args>
 #   py:<args>         python <args> (a tool script)
 #   tracepy:<args>    rocprofv3 --kernel-trace --memory-copy-trace --stats -- python3 <args>
-# Environment knobs (PR_CLASSES=..., PR_HOT_SLOTS=...) may prefix a step as KEY=VAL@step.
+# Environment variables may prefix a step as KEY=VAL@step (e.g. PR_LIB_PATH=... for an A/B build;
+# the library itself reads no environment: layout choices are bench.py options).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift
@@ -51,8 +51,6 @@ for step in "$@"; do
       python3 tools/pmc_summary.py $P 26 $P/pmc_spmv.json > $P/summary.log 2>&1 || exit 1 ;;
     counters)
       env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc $args --output-format csv -d $O/counters_$n -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $log 2>&1 || exit 1 ;;
-    diag)
-      env "${envs[@]}" timeout -k 10 400 python -u tools/diag_spmv.py $args > $log 2>&1 || exit 1 ;;
     py)
       env "${envs[@]}" timeout -k 10 500 python -u $args > $log 2>&1 || exit 1 ;;
     tracepy)

@@ -5,7 +5,7 @@ exchange vs whole slices, per-iteration time, and the ranks against the single-p
 
 Each part's exchange runs as device copies here; the numbers that matter for the RCCL path are
 the per-rank volumes (xchg_send / xchg_recv, doubles per iteration) and the pack/unpack cost.
-Set PR_EXCHANGE=allgather for the whole-slice A/B (read at build time).
+--allgather: the whole-slice exchange (build option exchange_allgather) for the A/B.
 """
 import argparse
 import json
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--parts", default="2,4,8")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--allgather", action="store_true")
     a = ap.parse_args()
     E = a.edge_factor << a.scale
     s = torch.empty(E, dtype=torch.int32, device="cuda")
@@ -38,7 +39,8 @@ def main():
 
     def run(P):
         parts = [sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, part=p,
-                                          n_parts=P, keep_canonical=False) for p in range(P)]
+                                          n_parts=P, keep_canonical=False,
+                                          options={"exchange_allgather": int(a.allgather)}) for p in range(P)]
         try:
             infos = [p.info() for p in parts]
             if P == 1:
@@ -76,7 +78,7 @@ def main():
         send = [i["xchg_send"] for i in infos]
         recv = [i["xchg_recv"] for i in infos]
         whole = [(P - 1) * (i["local_rows"] + 2) for i in infos]
-        print(json.dumps({"scale": a.scale, "parts": P, "mode": os.environ.get("PR_EXCHANGE", "sparse"),
+        print(json.dumps({"scale": a.scale, "parts": P, "mode": "allgather" if a.allgather else "sparse",
                           "ms_per_iter_all_parts_one_gpu": round(ms, 3), "max_rel_vs_1part": rel,
                           "xchg_recv_doubles": recv, "xchg_send_doubles": send,
                           "recv_frac_of_allgather": round(sum(recv) / max(sum(whole), 1), 4)}), flush=True)

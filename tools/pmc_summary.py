@@ -1,10 +1,12 @@
 """Summarise rocprofv3 CSVs from tools/gpu/run.sh (step pmc) into profiles/-ready JSON.
 
-usage: python tools/pmc_summary.py <prof_dir> <scale> [out_json]
-Reads <prof_dir>/trace/**/*kernel_stats.csv, <prof_dir>/fetch/**/*counter_collection.csv and
-<prof_dir>/write/**/*counter_collection.csv.  HBM bytes per k_spmv_units launch =
-2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes; the x2 is the gfx950 FETCH_SIZE half-count correction
-of MI355X_MICROARCH.md §HBM).
+usage: python tools/pmc_summary.py <prof_dir> [merge_json]
+Reads <prof_dir>/trace/**/*kernel_stats.csv (and the bench JSON line in <prof_dir>/trace.log for
+the workload and layout), <prof_dir>/fetch/**/*counter_collection.csv and
+<prof_dir>/write/**/*counter_collection.csv.  HBM bytes per launch of the pass's dominant kernel
+= 2 * FETCH_SIZE + WRITE_SIZE (KB -> bytes; the x2 is the gfx950 FETCH_SIZE half-count correction
+of MI355X_MICROARCH.md §HBM).  merge_json (profiles/pmc_spmv.json): one record per workload,
+keyed by bench.py's config.workload, under the bench's LAYOUT_VERSION.
 """
 import csv
 import glob
@@ -13,8 +15,8 @@ import os
 import sys
 
 # the SpMV pass of one iteration = these kernels (pr_iter.hip iter_compute)
-PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue")
-KERNEL = "k_spmv_hot"
+PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue", "k_spmv_rows")
+KERNEL = "k_spmv_hot"  # replaced by the pass kernel with the most time in the trace
 
 
 def rows(pattern):
@@ -25,7 +27,8 @@ def rows(pattern):
     return out
 
 
-def counter_per_launch(d, name, kernels=(KERNEL,)):
+def counter_per_launch(d, name, kernels=None):
+    kernels = kernels or (KERNEL,)
     vals = {}
     for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
         if not any(k in r.get("Kernel_Name", "") for k in kernels) or r.get("Counter_Name") != name:
@@ -45,17 +48,35 @@ def counter_per_pass(d, name):
             continue
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per[(key, kn)] = per.get((key, kn), 0.0) + float(r["Counter_Value"])
-    n_iter = len({k for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn}) or 1
+    ends = [kn for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn]
+    if ends:
+        n_iter = len({k for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn})
+    else:  # row-block layout: one k_spmv_rows launch per pass (bench line's rows passes)
+        n_iter = max(1, len({k for (k, kn) in per}) // max(1, ROWS_PASSES))
     return sum(per.values()) / n_iter if per else None
 
 
+ROWS_PASSES = 1
+
+
 def main():
-    d, scale = sys.argv[1], int(sys.argv[2])
-    out_json = sys.argv[3] if len(sys.argv) > 3 else None
+    global KERNEL, ROWS_PASSES
+    d = sys.argv[1]
+    merge = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else (sys.argv[3] if len(sys.argv) > 3 else None)
     stats = rows(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
-    summary = {"kernels": []}
-    for r in stats:
-        summary["kernels"].append({k: r[k] for k in r})
+    line = {}
+    try:
+        for ln in open(os.path.join(d, "trace.log")):
+            if ln.startswith("{"):
+                line = json.loads(ln)
+    except OSError:
+        pass
+    cfg = line.get("config", {})
+    ROWS_PASSES = int((line.get("roofline") or {}).get("launches_per_pass") or 1)
+    pass_stats = [r for r in stats if any(k in r.get("Name", "") for k in PASS_KERNELS)]
+    if pass_stats:
+        top = max(pass_stats, key=lambda r: float(r["TotalDurationNs"]))
+        KERNEL = top["Name"].split("(")[0].split("<")[0].replace("void ", "").replace("pr::", "")
     spmv = [r for r in stats if KERNEL in r.get("Name", "")]
     hit = counter_per_launch(os.path.join(d, "l2"), "TCC_HIT_sum")
     miss = counter_per_launch(os.path.join(d, "l2"), "TCC_MISS_sum")
@@ -64,13 +85,15 @@ def main():
     import re
     bench_src = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "bench.py")).read()
     res = {
-        "workload": f"R-MAT scale-{scale} edge-factor 16 (Graph500 .57/.19/.19, seed 2)",
+        "workload": cfg.get("workload"),
+        "layout": cfg.get("layout"),
         "layout_version": re.search(r'LAYOUT_VERSION = "([^"]+)"', bench_src).group(1),
         "kernel": KERNEL,
         "trace_avg_ns": float(spmv[0]["AverageNs"]) if spmv else None,
         "trace_calls": int(spmv[0]["Calls"]) if spmv else None,
         "fetch_size_kb_median": fetch[len(fetch) // 2] if fetch else None,
         "write_size_kb_median": write[len(write) // 2] if write else None,
+        "bench_ms_per_step": line.get("ms_per_step"),
     }
     if hit and miss:
         h, m = hit[len(hit) // 2], miss[len(miss) // 2]
@@ -86,12 +109,18 @@ def main():
         res["hbm_bytes_per_pass"] = (2 * fp + wp) * 1024
         res["pass_kernels"] = list(PASS_KERNELS)
     res["trace_pass_kernels"] = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
-                                 for r in stats if any(k in r.get("Name", "") for k in PASS_KERNELS)}
+                                 for r in pass_stats}
     print(json.dumps(res, indent=1))
-    print(json.dumps(summary["kernels"][:12], indent=1))
-    if out_json:
-        with open(out_json, "w") as f:
-            json.dump(res, f, indent=1)
+    if merge:
+        db = {}
+        if os.path.exists(merge):
+            with open(merge) as f:
+                db = json.load(f)
+        if db.get("layout_version") != res["layout_version"] or "workloads" not in db:
+            db = {"layout_version": res["layout_version"], "workloads": {}}
+        db["workloads"][res["workload"]] = res
+        with open(merge, "w") as f:
+            json.dump(db, f, indent=1)
 
 
 if __name__ == "__main__":
