@@ -45,7 +45,7 @@ sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 METRIC = "PageRank GTEPS/iter + % HBM roofline, R-MAT scale-26 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 # bumped whenever the SpMV pass changes, so a stale rocprof traffic figure is never reported
-LAYOUT_VERSION = "r3-split-c64-grpepi-walk-narrow+rows-t1024-r17-v10"
+LAYOUT_VERSION = "r3-split-c64-grpepi-walk-narrow-v10"
 
 
 def log(msg: str) -> None:
@@ -179,7 +179,7 @@ def main() -> int:
     ap.add_argument("--graph", choices=["rmat", "er", "lj", "twitter"], default="rmat",
                     help="lj / twitter: the Chung-Lu shapes of BASELINE.json configs[1] / [4]")
     ap.add_argument("--seed", type=int, default=None)
-    ap.add_argument("--layout", choices=["auto", "fused", "split", "rows"], default="auto",
+    ap.add_argument("--layout", choices=["auto", "fused", "split"], default="auto",
                     help="graph layout (A/B; auto picks by gather-space size)")
     ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (no cpu_baseline, no parity)")
     ap.add_argument("--parity-iters", type=int, default=10, help="K of the parity / cpu_baseline leg (Sparky.java:187)")
@@ -417,7 +417,7 @@ def main() -> int:
                 "exchange_doubles_per_iter_rank0": info.get("xchg_send", 0) if world > 1 else 0,
                 "iterations_timed": a.steps,
                 "build_options": bopts or None,
-                "layout": ["fused", "split", "rows"][info.get("layout", 0)],
+                "layout": ["fused", "split"][info.get("layout", 0)],
                 "hot_cover": round(info.get("hot_cover_ppm", 0) / 1e6, 4),
             },
             "roofline": {
@@ -429,12 +429,10 @@ def main() -> int:
                 "traffic": pmc_traffic(workload) if world == 1 else None,
                 "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue_grp (split layout, {info.get('classes')} "
                            "column classes, run per XCD in phases)" if info.get("layout") == 1
-                           else ("spmv pass: k_spmv_rows (row-block layout, LDS row sums, update fused)"
-                                 if info.get("layout") == 2 else "spmv pass: k_spmv_units (fused layout)")),
+                           else "spmv pass: k_spmv_units (fused layout)"),
                 "classes": info.get("classes"),
                 "bytes_model": "12*E'_part + 36*V_part per launch (pull-fp64-v1)",
                 "spmv_ms_mean": round(spmv_ms, 4),
-                "launches_per_pass": info.get("launches", 1),
                 "iter_ms_mean_events": round(st["iter_ms_mean"], 4),
                 "exchange_ms_mean": round(st["exchange_ms_mean"], 4),
             },

@@ -44,7 +44,6 @@ extern "C" {
 #define PR_NO_CANONICAL 4u   /* drop the canonical CSR after the build (no export)        */
 #define PR_LAYOUT_FUSED 8u   /* force the single-pass layout (default: chosen by size)    */
 #define PR_LAYOUT_SPLIT 16u  /* force the per-XCD column-class layout                     */
-#define PR_LAYOUT_ROWS 32u   /* force the row-block layout (LDS row sums, no partial slots)  */
 
 /* ---- vertex flag bits (pr_graph_export_csr vflags) ---------------------------------- */
 #define PR_VF_KEY 1u    /* vertex is a record key / src          Sparky.java:127-135      */
@@ -71,13 +70,12 @@ extern "C" {
 #define PR_INFO_XCHG_RECV 15   /* doubles this part receives per iteration (P > 1)        */
 #define PR_INFO_PARTIAL_SLOTS 16 /* (row, column class) segment sums of the split layout     */
 #define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
-#define PR_INFO_EPILOGUE 18    /* 0 fused units, 3 grouped (split), 4 fused into row tiles   */
+#define PR_INFO_EPILOGUE 18    /* 0 fused units, 3 grouped (split)                           */
 #define PR_INFO_GATHER_EST 19  /* bytes of the part's expected gather space (class policy)   */
 #define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
-#define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots), 2 rows  */
+#define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots)          */
 #define PR_INFO_HOT_COVER 22   /* in-links read from the LDS hot sets, parts per million      */
-#define PR_INFO_LAUNCHES 23    /* launches of the dominant SpMV kernel per iteration (row-block passes) */
-#define PR_INFO_COUNT 24
+#define PR_INFO_COUNT 23
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */

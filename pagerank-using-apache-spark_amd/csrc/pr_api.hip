@@ -46,7 +46,6 @@ size_t pr_graph::device_bytes() const {
   b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
-  b += tile_u.bytes + rcodes.bytes + rrows.bytes;
   return b;
 }
 
@@ -125,10 +124,9 @@ int create_common(int32_t device, int32_t part, int32_t n_parts, int32_t n_verti
   if (n_parts > pr::kMaxParts) return fail(PR_ERR_INVALID, "n_parts above 64 is not supported");
   if (n_vertices < 0 || n_edges < 0) return fail(PR_ERR_INVALID, "negative size");
   if (n_edges > 0 && (!src || !dst)) return fail(PR_ERR_INVALID, "src/dst is NULL");
-  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT | PR_LAYOUT_ROWS))
+  if (flags & ~(PR_DANGLING_NONE | PR_INPUT_DEVICE | PR_NO_CANONICAL | PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT))
     return fail(PR_ERR_INVALID, "unknown flag bits");
-  const uint32_t lay = flags & (PR_LAYOUT_FUSED | PR_LAYOUT_SPLIT | PR_LAYOUT_ROWS);
-  if (lay & (lay - 1)) return fail(PR_ERR_INVALID, "PR_LAYOUT_FUSED / _SPLIT / _ROWS are exclusive");
+  if ((flags & PR_LAYOUT_FUSED) && (flags & PR_LAYOUT_SPLIT)) return fail(PR_ERR_INVALID, "PR_LAYOUT_FUSED and PR_LAYOUT_SPLIT are exclusive");
   pr_build_opts opts;
   PR_TRY(parse_options(options, n_options, &opts));
   PR_TRY(check_device(device));
@@ -205,13 +203,12 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
   if (!g || !info) return fail(PR_ERR_INVALID, "NULL argument");
   const int64_t v[PR_INFO_COUNT] = {g->V,        g->E_dedup,  g->n_sink,    g->n_nolink, g->n_indeg0,
                                     g->max_indeg, g->n_local,  g->local_nnz, g->part,     g->nparts,
-                                    g->n_units + g->n_hunits + g->n_runits, g->n_long + g->n_segs,
+                                    g->n_units + g->n_hunits, g->n_long + g->n_segs,
                                     (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->layout == pr::kLayoutRows ? 4 : (g->C == 1 ? 0 : 3), g->gather_est,
-                                    g->n_walk_groups, g->layout, g->hot_cover_ppm,
-                                    g->layout == pr::kLayoutRows ? g->rows_passes : 1};
+                                    g->C == 1 ? 0 : 3, g->gather_est, g->n_walk_groups, g->layout,
+                                    g->hot_cover_ppm};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

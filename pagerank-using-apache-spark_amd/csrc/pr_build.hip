@@ -128,16 +128,6 @@ __global__ void k_reader_est(int32_t V, int P, const int32_t *__restrict__ deg, 
   atomicAdd(sum, acc);
 }
 
-// Out-degree sum of the first n vertices of the degree order (the layout policy's estimate of the
-// in-links the split layout's LDS hot sets would serve).
-__global__ void k_top_degree_sum(int64_t n, int b, uint64_t maxd, const uint64_t *__restrict__ sorted_vk,
-                                 unsigned long long *__restrict__ sum) {
-  unsigned long long acc = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    acc += maxd - (sorted_vk[i] >> b);
-  atomicAdd(sum, acc);
-}
-
 // Internal order key: out-degree descending, original ID ascending (hot contributions first).
 __global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__restrict__ deg,
                              uint64_t *__restrict__ vk) {
@@ -186,53 +176,6 @@ struct PartXform {
     return (seg << (brow + bg)) | (row << bg) | (uint64_t)gs;
   }
 };
-
-// Row-block layout (pr_rows.h): (row << bg) | gather position -> the sweep key
-// (tile, region, row within the tile, position within the region), the position mapped into the
-// compacted gather space first (cmap, P > 1); *bad counts sources the exchange lists miss.
-__global__ void k_rows_rekey(int64_t n, uint64_t *__restrict__ keys, int bg, const int32_t *__restrict__ cmap,
-                             unsigned long long *__restrict__ bad) {
-  constexpr int sh = kRowsRegionShift, bt = kRowsTileBits;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[i];
-    const uint64_t row = k >> bg;
-    int64_t gs = (int64_t)(k & ((uint64_t(1) << bg) - 1));
-    if (cmap) {
-      gs = cmap[gs];
-      if (gs < 0) {
-        atomicAdd(bad, 1ull);
-        gs = 0;
-      }
-    }
-    const uint64_t tile = row >> bt, rit = row & (kRowsTile - 1);
-    const int bp = bg > sh ? bg : sh;  // position bits (a region may exceed a small gather space)
-    keys[i] = (tile << (bp + bt)) | (((uint64_t)gs >> sh) << (sh + bt)) | (rit << sh) |
-              ((uint64_t)gs & ((uint64_t(1) << sh) - 1));
-  }
-}
-
-// Row-block layout: entry i of the sorted sweep keys -> its code (byte offset | segment end) and row
-// within the tile, at its place in the tile's padded unit stream.  A segment ends where (tile,
-// region, row) changes, at the tile's last entry and at every unit's last entry.
-__global__ void k_rows_fill(int64_t n, const uint64_t *__restrict__ keys, int bg, const int64_t *__restrict__ tile_beg,
-                            const int64_t *__restrict__ tile_u, uint32_t *__restrict__ codes,
-                            uint16_t *__restrict__ rows) {
-  constexpr int sh = kRowsRegionShift, bt = kRowsTileBits;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t key = keys[i];
-    const int bp = bg > sh ? bg : sh;
-    const int64_t t = (int64_t)(key >> (bp + bt));
-    const int64_t k = i - tile_beg[t];
-    const int64_t p = tile_u[t] * kWaveUnit + k;
-    const uint64_t rit = (key >> sh) & (kRowsTile - 1);
-    const uint64_t pos = (((key >> (sh + bt)) & ((uint64_t(1) << (bp - sh)) - 1)) << sh) |
-                         (key & ((uint64_t(1) << sh) - 1));
-    const bool last = i + 1 == tile_beg[t + 1];
-    const bool end = last || (k % kWaveUnit) == kWaveUnit - 1 || (keys[i + 1] >> sh) != (key >> sh);
-    codes[p] = (uint32_t)(pos * 8) | (end ? 1u : 0u);
-    rows[p] = (uint16_t)rit;
-  }
-}
 
 // row_ptr over rows [0, R) of keys[lo, hi) whose row is (key >> shift) & rmask.
 __global__ void k_row_ptr_seg(const uint64_t *__restrict__ keys, int64_t lo, int64_t hi, int shift,
@@ -439,65 +382,6 @@ static int hot_slots_setting(const pr_build_opts &o) {
   return std::max(0, std::min(k, kHotSlotsMax));
 }
 
-// Row-block layout plan (pr_rows.h): keys hold the part's in-links as (local row << bg) | gather
-// position; re-keyed to (tile, region, row within the tile, position) and sorted, they become
-// every tile's sweep stream, cut into kWaveUnit-entry units padded per tile.
-static int plan_rows(pr_graph *g, uint64_t *keys, uint64_t *tmp, int64_t lm, int bg, const int32_t *cmap) {
-  hipStream_t s = g->stream;
-  const unsigned T = 256;
-  const int64_t nt = (g->n_rows + kRowsTile - 1) / kRowsTile;
-  const int bp = std::max(bg, kRowsRegionShift);  // the sweep key's position bits (k_rows_rekey)
-  g->n_tiles = nt;
-  if (lm > 0) {
-    DevBuf bad;
-    PR_TRY(bad.alloc(sizeof(unsigned long long)));
-    PR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_rows_rekey, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s, lm, keys, bg, cmap,
-                       bad.as<unsigned long long>());
-    PR_HIP(hipGetLastError());
-    unsigned long long hb = 0;
-    PR_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(hb), hipMemcpyDeviceToHost, s));
-    PR_HIP(hipStreamSynchronize(s));
-    if (hb) return fail(PR_ERR_STATE, "exchange lists miss a source of this part's in-links");
-    PR_TRY(radix_sort_u64(keys, tmp, lm, 0, bp + kRowsTileBits + bits_for((uint64_t)nt), s));
-  }
-  DevBuf beg;
-  PR_TRY(beg.alloc(sizeof(int64_t) * (size_t)(nt + 1)));
-  hipLaunchKernelGGL(k_row_ptr_seg, dim3(grid_for(lm + 1, T, 65536)), dim3(T), 0, s, keys, (int64_t)0, lm,
-                     bp + kRowsTileBits, ~uint64_t(0), nt, beg.as<int64_t>());
-  PR_HIP(hipGetLastError());
-  std::vector<int64_t> hb((size_t)nt + 1), hu((size_t)nt + 1);
-  PR_HIP(hipMemcpyAsync(hb.data(), beg.p, sizeof(int64_t) * hb.size(), hipMemcpyDeviceToHost, s));
-  PR_HIP(hipStreamSynchronize(s));
-  int64_t nu = 0;
-  for (int64_t t = 0; t < nt; ++t) {
-    hu[t] = nu;
-    nu += (hb[t + 1] - hb[t] + kWaveUnit - 1) / kWaveUnit;
-  }
-  hu[nt] = nu;
-  g->n_runits = nu;
-  PR_TRY(g->tile_u.alloc(sizeof(int64_t) * hu.size()));
-  PR_HIP(hipMemcpyAsync(g->tile_u.p, hu.data(), sizeof(int64_t) * hu.size(), hipMemcpyHostToDevice, s));
-  const int64_t ne = nu * kWaveUnit;
-  PR_TRY(g->rcodes.alloc(sizeof(uint32_t) * (size_t)(ne > 0 ? ne : 1)));
-  PR_TRY(g->rrows.alloc(sizeof(uint16_t) * (size_t)(ne > 0 ? ne : 1)));
-  // padding: an out-of-range offset (no memory request) without an end mark, row 0
-  PR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g->rcodes.p), 0xFFFFFFF0u, (size_t)(ne > 0 ? ne : 1), s));
-  PR_HIP(hipMemsetAsync(g->rrows.p, 0, sizeof(uint16_t) * (size_t)(ne > 0 ? ne : 1), s));
-  if (lm > 0)
-    hipLaunchKernelGGL(k_rows_fill, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s, lm, keys, bg, beg.as<int64_t>(),
-                       g->tile_u.as<int64_t>(), g->rcodes.as<uint32_t>(), g->rrows.as<uint16_t>());
-  PR_HIP(hipGetLastError());
-  int n_cu = 0;
-  PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
-  g->rows_grid = std::max(1, n_cu * kRowsWgPerCu);
-  const int64_t waves = (int64_t)g->rows_grid * kRowsWaves;
-  g->rows_passes = (int)std::max<int64_t>(1, (nt + waves - 1) / waves);
-  PR_TRY(prepare_hot_kernel());
-  PR_HIP(hipStreamSynchronize(s));
-  return PR_OK;
-}
-
 int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *dst_in) {
   static_assert(kMaxClasses == 16 * kXcds, "class counts");
   auto t_start = std::chrono::steady_clock::now();
@@ -617,28 +501,15 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(radix_sort_u64(vk.as<uint64_t>(), vtmp.as<uint64_t>(), V, 0, b + bd, s));
   }
   vtmp.reset();
-  // Layout policy: the fused layout while the gather space fits the L2s; beyond, the split layout
-  // (column classes with LDS hot sets) unless its hot sets would serve fewer than kRowsMaxHotCover
-  // of the in-links (uniform graphs) -- then the row-block layout, which keeps row sums in LDS and
-  // writes no partial slots.  The hot sets hold the top c_split * slots sources of the degree order.
+  // Layout policy: the fused layout while the gather space fits the L2s, the split layout beyond
+  // (profiles/r03/rows_layout/: a row-block layout with LDS row sums and no partial slots ran 2x
+  // slower at ER s24 and far slower on skewed graphs, and was removed)
   const int c_split = class_setting(g->opts, gather_est);
   const bool big = (int64_t)P * g->n_local_max * 8 > kSplitMinSliceBytes;
   int layout = big ? kLayoutSplit : kLayoutFused;
-  if (kRowsMaxHotCover > 0.0 && big && !(g->flags & (PR_LAYOUT_SPLIT | PR_LAYOUT_FUSED)) && m > 0) {
-    const int64_t n_hot = std::min<int64_t>(V, (int64_t)c_split * hot_slots_setting(g->opts));
-    PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(k_top_degree_sum, dim3(grid_for(n_hot, T, 1024)), dim3(T), 0, s, n_hot, b, maxd,
-                       vk.as<uint64_t>(), cnt.as<unsigned long long>());
-    PR_HIP(hipGetLastError());
-    unsigned long long top = 0;
-    PR_HIP(hipMemcpyAsync(&top, cnt.p, sizeof(top), hipMemcpyDeviceToHost, s));
-    PR_HIP(hipStreamSynchronize(s));
-    if ((double)top < kRowsMaxHotCover * (double)m) layout = kLayoutRows;
-  }
   if (g->flags & PR_LAYOUT_FUSED) layout = kLayoutFused;
   if (g->flags & PR_LAYOUT_SPLIT) layout = kLayoutSplit;
-  if (g->flags & PR_LAYOUT_ROWS) layout = kLayoutRows;
-  // split and row-block entry codes are byte offsets below 2^31 (pr_internal.h)
+  // split-layout entry codes are byte offsets below 2^31 (pr_internal.h)
   if ((int64_t)P * (g->n_local_max + 64 + kMaxClasses) * 8 >= (1ll << 31) - (1ll << 20)) layout = kLayoutFused;
   int C = layout == kLayoutSplit ? c_split : 1;
   g->layout = layout;
@@ -675,11 +546,11 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                        keys.as<uint64_t>(), &lm, s));
   g->local_nnz = lm;
   PR_TRY(radix_sort_u64(keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, 0, bg + brow + bseg, s));
-  PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 && layout != kLayoutRows ? lm : 1)));
-  if (lm > 0 && layout != kLayoutRows)
+  PR_TRY(g->col.alloc(sizeof(int32_t) * (lm > 0 ? lm : 1)));
+  if (lm > 0)
     hipLaunchKernelGGL(k_local_col, dim3(grid_for(lm, T, 65536)), dim3(T), 0, s,
                        keys.as<uint64_t>(), lm, maskg, g->col.as<int32_t>());
-  if (cmap.p && lm > 0 && layout != kLayoutRows) {  // columns -> the compacted gather space (order within rows kept)
+  if (cmap.p && lm > 0) {  // columns -> the compacted gather space (order within rows kept)
     DevBuf bad;
     PR_TRY(bad.alloc(sizeof(unsigned long long)));
     PR_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
@@ -711,12 +582,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   int64_t pieces = 0;
   g->nblk = (R + 63) / 64;
   std::vector<int64_t> poff(kMaxClasses + 1, 0);
-  if (layout == kLayoutRows) {
-    PR_TRY(plan_rows(g, keys.as<uint64_t>(), tmp.as<uint64_t>(), lm, bg, cmap.p ? cmap.as<int32_t>() : nullptr));
-    keys.reset();
-    tmp.reset();
-    seg_p0.push_back(0);
-  } else if (C == 1) {
+  if (C == 1) {
     // fused layout: one CSR over all rows, 256-thread units with the fused epilogue
     DevBuf rp_dev;
     PR_TRY(rp_dev.alloc(sizeof(int64_t) * ((size_t)R + 1)));
@@ -783,7 +649,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipGetLastError());
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
-    g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
+    // one 1024-thread workgroup per CU; two when a smaller hot set (PR_BOPT_HOT_SLOTS) leaves room
+    // for a second workgroup's LDS (32 waves per CU)
+    const int wg_per_cu = hg.lds_bytes() * 2 <= (size_t)kHotLdsBytes ? 2 : 1;
+    g->hot_grid = std::max(C, n_cu * wg_per_cu / C * C);  // C | grid: every class gets the same CUs
     g->hot_grid_full = g->hot_grid;
     PR_TRY(set_hot_reserve(g, g->opts.hot_reserve));
 
@@ -863,8 +732,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->epi_narrow = epi_narrow_ok(C) && (g->opts.epi_narrow < 0 ? auto_narrow : g->opts.epi_narrow != 0);
     g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
   }
-  if (layout == kLayoutRows) g->ep_blocks = g->rows_grid * g->rows_passes;  // k_spmv_rows' block partials
-  // finalize input: fused-unit partials, the split epilogue's or the row-block passes' block partials
+  // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 

@@ -53,7 +53,7 @@ struct pr_graph {
   int part = 0, nparts = 1;
   int64_t n_local = 0;      // rows owned (without holes)
   int64_t n_rows = 0;       // C * Q_pad local rows (with holes)
-  int layout = 0;           // pr::kLayoutFused / kLayoutSplit / kLayoutRows
+  int layout = 0;           // pr::kLayoutFused / kLayoutSplit
   int C = 1;                // column classes (split layout; 1 otherwise)
   int64_t gather_est = 0;   // expected gather-space bytes the class count was chosen from
   int64_t Q_pad = 0;        // rows per class region
@@ -90,11 +90,6 @@ struct pr_graph {
   pr::DevBuf eoff, epos;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   int64_t hot_cover_ppm = 0;  // in-links whose source is in a class's hot set (layout policy input)
-  // row-block layout (pr_rows.h): per tile its first unit (tile_u[n_tiles] = all units), per
-  // entry its code and row within the tile (kWaveUnit entries per unit, padded per tile)
-  pr::DevBuf tile_u, rcodes, rrows;
-  int64_t n_tiles = 0, n_runits = 0;
-  int rows_grid = 0, rows_passes = 0;
   pr::DevBuf cbuf[2];
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;

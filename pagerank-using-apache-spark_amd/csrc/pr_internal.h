@@ -75,7 +75,6 @@ inline unsigned grid_for(int64_t n, int threads, unsigned cap = 1u << 20) {
 // ---- layouts (pr_graph.h) -----------------------------------------------------------------------
 constexpr int kLayoutFused = 0;  // one class, k_spmv_units (gather space <= 4 MiB)
 constexpr int kLayoutSplit = 1;  // column classes, LDS hot sets, partial slots (k_spmv_hot + k_epilogue_grp)
-constexpr int kLayoutRows = 2;   // row tiles with LDS row sums (k_spmv_rows)
 
 // ---- SpMV work plan ------------------------------------------------------------------------
 // A unit is one workgroup of the SpMV launch.  STREAM: whole rows [r0, r0+meta) whose in-links
@@ -150,29 +149,6 @@ constexpr int kStageSlots = 128;
 constexpr int kHotLdsBytes = 160 * 1024;
 constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 2;
 constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18430 hot contributions (144 KiB)
-
-// ---- row-block layout (pr_rows.h k_spmv_rows) ---------------------------------------------------
-// A tile of kRowsTile local rows belongs to one wave for a pass; its row sums live in LDS.
-// (PR_ROWS_TILE_BITS / PR_ROWS_REGION_SHIFT: -D overrides for A/B builds of the library only)
-#ifndef PR_ROWS_TILE_BITS
-#define PR_ROWS_TILE_BITS 10
-#endif
-#ifndef PR_ROWS_REGION_SHIFT
-#define PR_ROWS_REGION_SHIFT 17
-#endif
-constexpr int kRowsTileBits = PR_ROWS_TILE_BITS;
-constexpr int kRowsTile = 1 << kRowsTileBits;   // rows per tile (8 KiB of fp64 sums)
-constexpr int kRowsWaves = 16;                  // waves per workgroup
-constexpr int kRowsThreads = kRowsWaves * 64;
-constexpr int kRowsRegionShift = PR_ROWS_REGION_SHIFT;  // sweep regions of 2^17 contributions (1 MiB)
-constexpr int kRowsLdsBytes = 8 * kRowsWaves * kRowsTile + 16 * kRowsWaves;
-// workgroups per CU: as many as the LDS holds, at most two (32 waves per CU)
-constexpr int kRowsWgPerCu = (160 * 1024) / kRowsLdsBytes >= 2 ? 2 : 1;
-// the layout policy would route a graph to the row-block layout when the split layout's LDS hot
-// sets serve fewer than this share of its in-links; 0 = never (measured: ER s24 runs 3.95 ms per
-// iteration in row tiles against 1.98 ms split -- the tiles' sweeps do not keep an XCD's waves in
-// one L2-sized region, so nearly every gather misses L2)
-constexpr double kRowsMaxHotCover = 0.0;
 
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {

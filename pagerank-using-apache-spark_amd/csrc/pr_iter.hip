@@ -27,7 +27,6 @@
 
 #include "pr_device.h"
 #include "pr_graph.h"
-#include "pr_rows.h"
 #include "pr_spmv.h"
 
 namespace pr {
@@ -162,8 +161,6 @@ int prepare_hot_kernel() {
       }
   PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot), hipFuncAttributeMaxDynamicSharedMemorySize,
                              kHotLdsBytes));
-  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_rows), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             kRowsLdsBytes));
   return PR_OK;
 }
 
@@ -290,21 +287,13 @@ int iter_compute(pr_graph *g) {
   }
   // light rows (all rows when C == 1): fused single pass
   if (g->C == 1) PR_TRY(join_exchange(g));
-  if (g->layout == kLayoutRows) {  // row tiles: one launch per pass, the update fused (pr_rows.h)
-    for (int p = 0; p < g->rows_passes; ++p)
-      hipLaunchKernelGGL(k_spmv_rows, dim3((unsigned)g->rows_grid), dim3(kRowsThreads), kRowsLdsBytes, s, p,
-                         g->n_tiles, g->tile_u.as<int64_t>(), g->rcodes.as<uint32_t>(), g->rrows.as<uint16_t>(),
-                         g->cbuf[in].as<double>(), (uint32_t)(sizeof(double) * g->gsize),
-                         g->cbuf[out].as<double>() + own, g->r.as<double>(), g->rowinfo.as<uint32_t>(), g->n_rows,
-                         g->slots, (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>());
-  }
   if (g->n_units > 0)
     hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
                        g->cbuf[in].as<double>(), g->cbuf[out].as<double>() + own, g->r.as<double>(),
                        g->rowinfo.as<uint32_t>(), g->piece_part.as<double>(), g->unit_part.as<double2>(),
                        g->slots, g->S_pad, (double)g->V, g->teleport, g->damping);
-  int64_t n_parts = g->layout == kLayoutRows ? g->ep_blocks : g->n_units;
+  int64_t n_parts = g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
     const int nph = n_hot_phases(g);
     if (g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1) {

@@ -7,7 +7,6 @@
 //                   classes one after another (phases)
 //   k_seg_reduce    split layout: long segments summed from their pieces in piece order
 //   k_epilogue_grp  split layout: per row its segment sums in class order, then the update
-//   (the row-block layout's kernel, k_spmv_rows, is in pr_rows.h)
 //
 // Every sum has a fixed order: results are bitwise reproducible.  A/B variants of these kernels
 // are built as separate libraries (PR_LIB_PATH), never compiled into the product.

@@ -66,8 +66,8 @@ class PageRankGraph:
                  options: Optional[dict] = None):
         """src/dst: int32 host arrays (numpy) of raw interned edges, dst == -1 for a record
         without links; or, with device_input=True, integer device addresses (e.g. from
-        torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (the size and hot-set policy),
-        'fused', 'split' (column classes) or 'rows' (row tiles) (pr_graph.h).  options: build
+        torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (column classes once the
+        contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h).  options: build
         options of pr_graph_create_ex by name (_lib.BUILD_OPTIONS: classes, hot_slots,
         exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow)."""
         L = _lib.load()
@@ -82,10 +82,8 @@ class PageRankGraph:
             flags |= _lib.PR_LAYOUT_FUSED
         elif layout == "split":
             flags |= _lib.PR_LAYOUT_SPLIT
-        elif layout == "rows":
-            flags |= _lib.PR_LAYOUT_ROWS
         elif layout != "auto":
-            raise ValueError("layout must be 'auto', 'fused', 'split' or 'rows'")
+            raise ValueError("layout must be 'auto', 'fused' or 'split'")
         if device_input:
             flags |= _lib.PR_INPUT_DEVICE
             if n_edges is None:

@@ -40,7 +40,7 @@ def test_constants_match_header():
 
     hdr = open(os.path.join(ROOT, "include", "pagerank_hip.h")).read()
     for name in ["PR_DANGLING_NONE", "PR_INPUT_DEVICE", "PR_NO_CANONICAL", "PR_LAYOUT_FUSED", "PR_LAYOUT_SPLIT",
-                 "PR_LAYOUT_ROWS", "PR_VF_KEY", "PR_VF_SINK",
+                 "PR_VF_KEY", "PR_VF_SINK",
                  "PR_VF_NOLINK", "PR_VF_INDEG0", "PR_CB_RANKS", "PR_COMM_ID_BYTES"]:
         v = int(re.search(rf"#define {name} \(?(\d+)u?\)?", hdr).group(1))
         assert getattr(L, name) == v, name

@@ -43,7 +43,7 @@ def run_both(hip, oracle_c, V, src, dst, iters, dangling="local", init=None, lay
     ref = oracle_c.run(csr, iters, dangling_none=(dangling == "none"), init=init, keep_history=True)
     with hip.PageRankGraph(V, src, dst, dangling=dangling, layout=layout, options=options) as g:
         if layout != "auto":
-            assert g.info()["layout"] == {"fused": 0, "split": 1, "rows": 2}[layout]
+            assert g.info()["layout"] == {"fused": 0, "split": 1}[layout]
             assert g.info()["classes"] in ((8, 16, 32, 64, 128) if layout == "split" else (1,))
         assert_csr_equal(g, csr)
         hist = []
@@ -98,7 +98,7 @@ def random_edges(rng, V, E, p_nolink=0.05, hub_frac=0.0):
     return src.astype(np.int32), dst.astype(np.int32)
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("V,E,seed", [(1, 1, 0), (17, 60, 1), (1000, 9000, 2), (50000, 800000, 3)])
 def test_random_graphs(hip, oracle_c, V, E, seed, layout):
     rng = np.random.default_rng(seed)
@@ -110,7 +110,7 @@ def test_random_graphs(hip, oracle_c, V, E, seed, layout):
         assert abs(stats[it].l1_delta - ref["l1"][it]) <= 1e-9 * max(ref["l1"][it], 1.0)
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_long_rows_and_unit_boundaries(hip, oracle_c, layout):
     """Hubs split into many 2048-in-link pieces, rows of exactly 2048 / 2049 in-links, and a
     run of > 1024 short rows (the per-unit row cap)."""
@@ -129,16 +129,14 @@ def test_long_rows_and_unit_boundaries(hip, oracle_c, layout):
     assert indeg[1] == 2048 and indeg[2] == 2049 and indeg[4] == 2047
     if layout == "fused":
         assert info["n_long_rows"] == int(np.sum(indeg > 2048)) == 4  # 70000, 2049, 4096, 6144
-    elif layout == "split":  # long (row, class) segments: the 70000-in-link hub splits into 8 long segments
+    else:  # long (row, class) segments: the 70000-in-link hub splits into 8 long segments
         assert info["n_long_rows"] >= 8
-    else:  # row tiles: a hub's in-links are cut at unit ends, every piece added to its LDS row sum
-        assert info["layout"] == 2 and info["n_long_rows"] == 0 and info["epilogue"] == 4
     assert info["max_indeg"] == 70000
     for it in range(8):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_heavy_hub_and_many_indeg0(hip, oracle_c, layout):
     rng = np.random.default_rng(4)
     src, dst = random_edges(rng, 20000, 300000, p_nolink=0.2, hub_frac=0.3)
@@ -147,7 +145,7 @@ def test_heavy_hub_and_many_indeg0(hip, oracle_c, layout):
     assert max_rel(ranks, ref["ranks"]) <= RANK_TOL
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_dangling_none(hip, oracle_c, layout):
     rng = np.random.default_rng(5)
     src, dst = random_edges(rng, 3000, 20000)
@@ -167,7 +165,7 @@ def test_resume_from_saved_ranks(hip, oracle_c):
     assert max_rel(r3_2, r5) <= 1e-13
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_deterministic_bitwise(hip, layout):
     rng = np.random.default_rng(7)
     src, dst = random_edges(rng, 40000, 600000, hub_frac=0.05)
@@ -330,7 +328,7 @@ def test_rmat_s20_split_default_hot_set(hip, oracle_c):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_chunglu_generator_small(hip, oracle_c, layout):
     """The Chung-Lu generator (LJ / Twitter shapes) on a small instance with sink-only ranks and
     link-less records: raw labels in range, the link-less records present, interning equal to the
@@ -385,12 +383,10 @@ def test_lj_shaped_full_size(hip, oracle_c):
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
 
 
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 def test_compacted_gather_space_is_bitwise_whole_slices(hip, layout):
     """The compacted gather space (own slice + received runs) keeps every row's summation order,
-    so its ranks equal the whole-slice all-gather layout's bit for bit.  (Row tiles sweep their
-    in-links by region of the gather space, so there the order -- not the sums -- follows the
-    space: equal to rounding.)"""
+    so its ranks equal the whole-slice all-gather layout's bit for bit."""
     rng = np.random.default_rng(77)
     V = 30000
     src, dst = random_edges(rng, V, 300000, hub_frac=0.05)
@@ -404,14 +400,11 @@ def test_compacted_gather_space_is_bitwise_whole_slices(hip, layout):
         finally:
             for p in parts:
                 p.close()
-    if layout == "rows":
-        assert max_rel(out["sparse"], out["allgather"]) <= 1e-13
-    else:
-        assert np.array_equal(out["sparse"], out["allgather"])
+    assert np.array_equal(out["sparse"], out["allgather"])
 
 
 @pytest.mark.parametrize("xmode", ["sparse", "allgather"])
-@pytest.mark.parametrize("layout", ["fused", "split", "rows"])
+@pytest.mark.parametrize("layout", ["fused", "split"])
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode):
     """The row-partitioned path (layout + exchange) with P parts in one process on one GPU: the
@@ -567,53 +560,3 @@ def test_epilogue_narrow_workgroups(hip, oracle_c):
             assert np.array_equal(again, out[narrow])
     assert max_rel(out["1"], out["0"]) <= 1e-13
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
-
-
-
-def test_rows_layout_tiles(hip, oracle_c):
-    """The row-block layout (pr_rows.h k_spmv_rows, PR_LAYOUT_ROWS) on a uniform graph: the sums
-    have a fixed order (bitwise repeatable), no partial slots exist, and every iteration meets the
-    oracle bar -- with several passes (more tiles than waves) and tiles whose streams cross many
-    regions."""
-    rng = np.random.default_rng(2024)
-    V = 1_200_000  # > 4 MiB of contributions: beyond the fused layout; 1172 tiles
-    E = 16 * V
-    src = rng.integers(0, V, E).astype(np.int32)
-    dst = rng.integers(0, V, E).astype(np.int32)
-    seen = np.zeros(V, bool)
-    seen[src] = True
-    seen[dst] = True
-    miss = np.nonzero(~seen)[0].astype(np.int32)
-    src, dst = np.concatenate([src, miss]), np.concatenate([dst, np.full(miss.shape, -1, np.int32)])
-    csr = oracle_c.build_csr(V, src, dst)
-    ref = oracle_c.run(csr, 6, keep_history=True)
-    hist = []
-    with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="rows") as g:
-        info = g.info()
-        assert info["layout"] == 2 and info["epilogue"] == 4 and info["partial_slots"] == 0, info
-        r, st = g.run(6, want_ranks_in_callback=True, callback=lambda it, rr, ss: hist.append(rr))
-        again, _ = g.run(6)
-    assert np.array_equal(r, again)
-    for it in range(6):
-        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
-        assert abs(st[it].dangling_sum - ref["dc"][it]) <= RANK_TOL * max(ref["dc"][it], 1.0)
-        assert abs(st[it].l1_delta - ref["l1"][it]) <= RANK_TOL * max(ref["l1"][it], 1.0)
-
-
-@pytest.mark.parametrize("P", [2, 3])
-def test_rows_layout_partitioned(hip, oracle_c, P):
-    """Row tiles of a row partition: each part's sweep reads its compacted gather space (own slice
-    + received runs), with the exchange after every pass."""
-    rng = np.random.default_rng(55 + P)
-    V = 40000
-    src, dst = random_edges(rng, V, 600000, hub_frac=0.02)
-    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), 8)
-    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="rows")
-             for p in range(P)]
-    try:
-        assert all(p.info()["layout"] == 2 for p in parts)
-        r = hip.PartGroup(parts).run(8)
-    finally:
-        for p in parts:
-            p.close()
-    assert max_rel(r, ref["ranks"]) <= RANK_TOL

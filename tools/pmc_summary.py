@@ -15,7 +15,7 @@ import os
 import sys
 
 # the SpMV pass of one iteration = these kernels (pr_iter.hip iter_compute)
-PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue", "k_spmv_rows")
+PASS_KERNELS = ("k_spmv_units", "k_spmv_hot", "k_seg_reduce", "k_epilogue")
 KERNEL = "k_spmv_hot"  # replaced by the pass kernel with the most time in the trace
 
 
@@ -48,19 +48,12 @@ def counter_per_pass(d, name):
             continue
         key = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per[(key, kn)] = per.get((key, kn), 0.0) + float(r["Counter_Value"])
-    ends = [kn for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn]
-    if ends:
-        n_iter = len({k for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn})
-    else:  # row-block layout: one k_spmv_rows launch per pass (bench line's rows passes)
-        n_iter = max(1, len({k for (k, kn) in per}) // max(1, ROWS_PASSES))
+    n_iter = len({k for (k, kn) in per if "k_epilogue" in kn or "k_spmv_units" in kn}) or 1
     return sum(per.values()) / n_iter if per else None
 
 
-ROWS_PASSES = 1
-
-
 def main():
-    global KERNEL, ROWS_PASSES
+    global KERNEL
     d = sys.argv[1]
     merge = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else (sys.argv[3] if len(sys.argv) > 3 else None)
     stats = rows(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
@@ -72,7 +65,6 @@ def main():
     except OSError:
         pass
     cfg = line.get("config", {})
-    ROWS_PASSES = int((line.get("roofline") or {}).get("launches_per_pass") or 1)
     pass_stats = [r for r in stats if any(k in r.get("Name", "") for k in PASS_KERNELS)]
     if pass_stats:
         top = max(pass_stats, key=lambda r: float(r["TotalDurationNs"]))
