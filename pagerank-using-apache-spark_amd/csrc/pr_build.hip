@@ -649,10 +649,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipGetLastError());
     int n_cu = 0;
     PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
-    // one 1024-thread workgroup per CU; two when a smaller hot set (PR_BOPT_HOT_SLOTS) leaves room
-    // for a second workgroup's LDS (32 waves per CU)
-    const int wg_per_cu = hg.lds_bytes() * 2 <= (size_t)kHotLdsBytes ? 2 : 1;
-    g->hot_grid = std::max(C, n_cu * wg_per_cu / C * C);  // C | grid: every class gets the same CUs
+    g->hot_grid = std::max(C, n_cu / C * C);  // C | grid: every class gets the same CUs
     g->hot_grid_full = g->hot_grid;
     PR_TRY(set_hot_reserve(g, g->opts.hot_reserve));
 
