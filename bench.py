@@ -329,6 +329,8 @@ def main() -> int:
     bytes_launch = 12 * info["local_edges"] + 36 * info["local_rows"]
     achieved = bytes_launch / (spmv_ms * 1e-3) / 1e9 if spmv_ms > 0 else 0.0
 
+    tr = pmc_traffic(workload) if world == 1 else None
+
     # ---- validation leg (after the timed region): K iterations from a fresh reset vs the oracle ----
     cpu, parity = None, None
     wd.enter("parity", limits["parity"])
@@ -426,7 +428,10 @@ def main() -> int:
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(workload) if world == 1 else None,
+                # HBM bytes of one SpMV pass by rocprofv3 PMC (2 FETCH_SIZE + WRITE_SIZE), the unit of
+                # `achieved`; traffic_detail names the dominant kernel's own share
+                "traffic": (tr or {}).get("per_pass"),
+                "traffic_detail": tr,
                 "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue_grp (split layout, {info.get('classes')} "
                            "column classes, run per XCD in phases)" if info.get("layout") == 1
                            else "spmv pass: k_spmv_units (fused layout)"),

@@ -58,9 +58,37 @@ __global__ __launch_bounds__(256) void k_ta_probe(const double *__restrict__ tab
   }
   if (acc == 12345.0) out[t] = acc;
 }
+// CU-mask probe: every workgroup (one wave) records its XCC id and raw HW_ID register (CU, SH, SE
+// fields), so a stream's CU-mask bits can be mapped to physical CUs and XCDs.
+__global__ void k_cu_probe(uint32_t *__restrict__ out) {
+  uint32_t xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = xcc;
+    out[2 * blockIdx.x + 1] = hw;
+  }
+}
 }  // namespace
 
 extern "C" {
+
+// Launch nblocks one-wave workgroups on a stream created with the CU mask (nwords 32-bit words);
+// out: 2 words per workgroup (XCC id, HW_ID).
+int prd_cu_probe(int device, const uint32_t *mask, int nwords, int nblocks, uint32_t *out) {
+  PR_HIP(hipSetDevice(device));
+  hipStream_t st;
+  PR_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)nwords, mask));
+  uint32_t *d = nullptr;
+  PR_HIP(hipMalloc(&d, sizeof(uint32_t) * 2 * nblocks));
+  hipLaunchKernelGGL(k_cu_probe, dim3(nblocks), dim3(64), 0, st, d);
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipMemcpyAsync(out, d, sizeof(uint32_t) * 2 * nblocks, hipMemcpyDeviceToHost, st));
+  PR_HIP(hipStreamSynchronize(st));
+  (void)hipFree(d);
+  (void)hipStreamDestroy(st);
+  return 0;
+}
 
 // mode: 0 hipMalloc + plain loads, 1 nt, 2 sc1, 3 sc0|sc1, 4 uncached memory (hipDeviceMallocUncached),
 // 5 fine-grained memory (hipDeviceMallocFinegrained).  8 loads per thread.

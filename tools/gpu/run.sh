@@ -14,6 +14,7 @@
 #   counters:<c1,c2>  one rocprofv3 --pmc pass with these counters on bench.py --no-cpu-baseline
 #                     --steps 5 (respect the per-block limits: 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD)
 #   py:<args>         python <args> (a tool script)
+#   pmcpy:<c>:<args>  one rocprofv3 --pmc <c> pass over python <args> (a tool script)
 #   tracepy:<args>    rocprofv3 --kernel-trace --memory-copy-trace --stats -- python3 <args>
 # Environment variables may prefix a step as KEY=VAL@step (e.g. PR_LIB_PATH=... for an A/B build;
 # the library itself reads no environment: layout choices are bench.py options).
@@ -48,9 +49,12 @@ for step in "$@"; do
       env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o run -- python3 bench.py $A > $P/fetch.log 2>&1 && \
       env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o run -- python3 bench.py $A > $P/write.log 2>&1 && \
       env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $P/l2 -o run -- python3 bench.py $A > $P/l2.log 2>&1 && \
-      python3 tools/pmc_summary.py $P 26 $P/pmc_spmv.json > $P/summary.log 2>&1 || exit 1 ;;
+      python3 tools/pmc_summary.py $P $P/pmc_spmv.json > $P/summary.log 2>&1 || exit 1 ;;
     counters)
       env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc $args --output-format csv -d $O/counters_$n -o run -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $log 2>&1 || exit 1 ;;
+    pmcpy)  # pmcpy:<counter>:<python args>: one --pmc pass over a tool script
+      c=${arg%%:*}; rest=${arg#*:}
+      env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc $c --output-format csv -d $O/pmcpy_$n -o run -- python3 ${rest//,/ } > $log 2>&1 || exit 1 ;;
     py)
       env "${envs[@]}" timeout -k 10 500 python -u $args > $log 2>&1 || exit 1 ;;
     tracepy)
