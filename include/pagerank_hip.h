@@ -75,7 +75,8 @@ extern "C" {
 #define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
 #define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots)          */
 #define PR_INFO_HOT_COVER 22   /* in-links read from the LDS hot sets, parts per million      */
-#define PR_INFO_COUNT 23
+#define PR_INFO_CODE_BITS 23   /* bits per in-link of the split layout's entry codes: 20 compact, 32 */
+#define PR_INFO_COUNT 24
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */
@@ -122,12 +123,14 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
  * summation order.  An unknown key or an out-of-range value fails with PR_ERR_INVALID.  The library
  * reads no environment variables: every choice is an explicit option. */
 #define PR_BOPT_CLASSES 1     /* column classes of the split layout: 0 (size policy), 8, 16, 32, 64, 128 */
-#define PR_BOPT_HOT_SLOTS 2   /* LDS hot-set slots per class: -1 (default 18430) or 0..18430            */
+#define PR_BOPT_HOT_SLOTS 2   /* LDS hot-set slots per class: -1 (default 18429) or 0..18429            */
 #define PR_BOPT_EXCHANGE 3    /* P > 1: 0 per-peer runs (default), 1 whole-slice all-gather (all parts alike) */
 #define PR_BOPT_XCHG_CHUNKS 4 /* P > 1: 1 = the overlapped exchange from the start (PR_OPT_XCHG_CHUNKS) */
 #define PR_BOPT_HOT_RESERVE 5 /* CUs per XCD the heavy SpMV kernel leaves free, 0..3 (PR_OPT_HOT_RESERVE) */
 #define PR_BOPT_EPI_WALK 6    /* split layout: 1 (default) per-row walk of sparse epilogue groups, 0 never */
 #define PR_BOPT_EPI_NARROW 7  /* split layout: -1 auto (default), 0 four-wave, 1 one-wave epilogue workgroups */
+#define PR_BOPT_CODES 8       /* split layout: -1 (default) 2.5-byte entry codes where they fit (P = 1, class
+                                 regions < 2^19 positions), 0 always 4-byte codes; same sums either way */
 int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
                        const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
                        int32_t n_options, pr_graph **out);

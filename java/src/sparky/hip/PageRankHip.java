@@ -29,7 +29,7 @@ public final class PageRankHip implements AutoCloseable {
     /** pr_graph_create flags (include/pagerank_hip.h). */
     public static final int PR_DANGLING_LOCAL = 0, PR_DANGLING_NONE = 1, PR_NO_CANONICAL = 4;
     static final int PR_CB_RANKS = 1;
-    static final int PR_INFO_COUNT = 23;
+    static final int PR_INFO_COUNT = 24;
     /** PR_ABI_VERSION of include/pagerank_hip.h this binding was written against. */
     public static final int ABI_VERSION = 2;
 

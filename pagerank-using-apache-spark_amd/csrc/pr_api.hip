@@ -45,7 +45,7 @@ size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
   b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
-  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes;
+  b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes + cside.bytes;
   return b;
 }
 
@@ -87,7 +87,7 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
         o->classes = (int)v;
         break;
       case PR_BOPT_HOT_SLOTS:
-        if (v < -1 || v > pr::kHotSlotsMax) return fail(PR_ERR_INVALID, "PR_BOPT_HOT_SLOTS: -1 (default) or 0..18430");
+        if (v < -1 || v > pr::kHotSlotsMax) return fail(PR_ERR_INVALID, "PR_BOPT_HOT_SLOTS: -1 (default) or 0..18429");
         o->hot_slots = (int)v;
         break;
       case PR_BOPT_EXCHANGE:
@@ -107,6 +107,10 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
       case PR_BOPT_EPI_NARROW:
         if (v < -1 || v > 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_NARROW: -1 (auto), 0 or 1");
         o->epi_narrow = (int)v;
+        break;
+      case PR_BOPT_CODES:
+        if (v != -1 && v != 0) return fail(PR_ERR_INVALID, "PR_BOPT_CODES: -1 (compact where they fit) or 0 (32-bit)");
+        o->codes = (int)v;
         break;
       default:
         return fail(PR_ERR_INVALID, "unknown build option " + std::to_string(k));
@@ -208,7 +212,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
                                     g->C == 1 ? 0 : 3, g->gather_est, g->n_walk_groups, g->layout,
-                                    g->hot_cover_ppm};
+                                    g->hot_cover_ppm, g->C > 1 ? (g->code == pr::kCodeC20 ? 20 : 32) : 0};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

@@ -362,6 +362,55 @@ __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *_
   atomicAdd(n_hot, nh);
 }
 
+// Compact entry codes (pr_internal.h kCodeC20, P = 1): one thread per 8-entry lane group of a wave
+// unit writes the group's 8 u16 low index halves and its side word (end marks, high bits).  A
+// source at region offset o of class x (gather position x*Q_pad + o) has index o + 1; padding 0.
+// *n_hot counts the entries that read the LDS hot set; *bad the sources outside the unit's region
+// band (none by construction: the codes would then read another class's values).
+__global__ __launch_bounds__(64) void k_fill_c20(int64_t n_units, const Unit *__restrict__ units,
+                                                 const int64_t *__restrict__ src_off,
+                                                 const int32_t *__restrict__ n_real, const int32_t *__restrict__ col,
+                                                 int64_t Q_pad, int q_load, uint16_t *__restrict__ code16,
+                                                 uint32_t *__restrict__ cside, unsigned long long *n_hot,
+                                                 unsigned long long *bad) {
+  unsigned long long nh = 0, nb = 0;
+  for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
+    const Unit u = units[b];
+    const int64_t s0 = src_off[b];
+    const int n = n_real[b];
+    int64_t x0 = -1;  // the unit's class: the region of its first source
+    if (n > 0) x0 = (int64_t)(col[s0] & 0x7FFFFFFF) / Q_pad;
+    for (int grp = threadIdx.x; grp < u.n / 8; grp += 64) {
+      uint32_t side = 0, lo[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * grp + j;
+        uint32_t idx = 0;
+        if (i < n) {
+          const int32_t v = col[s0 + i];
+          const int64_t pos = v & 0x7FFFFFFF;
+          const int64_t x = pos / Q_pad;
+          nb += x != x0 ? 1 : 0;
+          idx = (uint32_t)(pos - x * Q_pad + 1);
+          nh += idx <= (uint32_t)q_load ? 1 : 0;
+          if (u.meta >= 0 && v < 0) side |= 1u << j;  // segment end (STREAM units)
+        }
+        lo[j] = idx & 0xFFFFu;
+        side |= ((idx >> 16) & 7u) << (8 + 3 * j);
+      }
+      uint4 q;
+      q.x = lo[0] | lo[1] << 16;
+      q.y = lo[2] | lo[3] << 16;
+      q.z = lo[4] | lo[5] << 16;
+      q.w = lo[6] | lo[7] << 16;
+      *reinterpret_cast<uint4 *>(code16 + (int64_t)u.p8 * 8 + 8 * grp) = q;
+      cside[(int64_t)u.p8 + grp] = side;
+    }
+  }
+  atomicAdd(n_hot, nh);
+  atomicAdd(bad, nb);
+}
+
 // Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the part's
 // gather space (its slice plus the expected received runs at P > 1) fits one XCD's 4 MiB L2 (the
 // phased schedule runs one class per XCD at a time), capped at kAutoMaxClasses; PR_BOPT_CLASSES
@@ -659,22 +708,40 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->hunits = std::move(sp.units);  // + the empty unit nu
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
-    PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
+    // compact codes when every region index fits (P = 1: a class's sources are its region of the
+    // one slice; a part of a row partition also reads received runs, so it keeps 32-bit codes)
+    const bool c20 = g->opts.codes != 0 && P == 1 && g->gsize == g->S_pad && g->Q_pad < (int64_t(1) << kC20IdxBits);
+    g->code = c20 ? kCodeC20 : kCodeU32;
+    if (c20) {
+      PR_TRY(g->colh.alloc(sizeof(uint16_t) * (sp.entries > 0 ? sp.entries : 8)));
+      PR_TRY(g->cside.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries / 8 : 1)));
+    } else {
+      PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
+      PR_TRY(g->cside.alloc(sizeof(uint32_t)));
+    }
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
     g->n_slots = poff[C];
     PR_HIP(hipMemcpyAsync(g->hucum.p, sp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     if (nu > 0) {
-      PR_HIP(hipMemsetAsync(cnt.p, 0, sizeof(unsigned long long), s));
-      hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
-                         g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
-                         hotidx.as<int32_t>(), g->colh.as<uint32_t>(), cnt.as<unsigned long long>());
+      PR_HIP(hipMemsetAsync(cnt.p, 0, 2 * sizeof(unsigned long long), s));
+      if (c20)
+        hipLaunchKernelGGL(k_fill_c20, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(64), 0, s, nu,
+                           g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
+                           g->col.as<int32_t>(), g->Q_pad, hg.q_load, g->colh.as<uint16_t>(),
+                           g->cside.as<uint32_t>(), cnt.as<unsigned long long>(), cnt.as<unsigned long long>() + 1);
+      else
+        hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
+                           g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
+                           g->col.as<int32_t>(), hotidx.as<int32_t>(), g->colh.as<uint32_t>(),
+                           cnt.as<unsigned long long>());
       PR_HIP(hipGetLastError());
-      unsigned long long n_hot = 0;
-      PR_HIP(hipMemcpyAsync(&n_hot, cnt.p, sizeof(n_hot), hipMemcpyDeviceToHost, s));
+      unsigned long long n_hot[2] = {0, 0};
+      PR_HIP(hipMemcpyAsync(n_hot, cnt.p, sizeof(n_hot), hipMemcpyDeviceToHost, s));
       PR_HIP(hipStreamSynchronize(s));
-      g->hot_cover_ppm = lm > 0 ? (int64_t)((double)n_hot * 1e6 / (double)lm) : 0;
+      if (n_hot[1]) return fail(PR_ERR_STATE, "compact codes: a unit reads outside its class region");
+      g->hot_cover_ppm = lm > 0 ? (int64_t)((double)n_hot[0] * 1e6 / (double)lm) : 0;
     }
     g->n_segs = sp.n_long;
     g->seg_slot = std::move(sp.seg_slot);

@@ -40,6 +40,7 @@ struct pr_build_opts {
   int hot_reserve = 0;
   bool epi_walk = true;
   int epi_narrow = -1;   // -1: by the share of walking groups
+  int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
 };
 
 struct pr_graph {
@@ -77,6 +78,10 @@ struct pr_graph {
   // segment of every 64-row block (cbase[blk][x]); long segments: pieces reduced in order into
   // partial[seg_slot[q]]; hpos[x * P*Kp + i]: gather position of LDS hot slot 1 + i of class x
   pr::DevBuf colh, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
+  // entry code format (pr_internal.h): kCodeU32 (colh = u32 codes) or kCodeC20 (colh = u16 low
+  // index bits, cside = one u32 of end marks and high bits per 8 entries)
+  int code = pr::kCodeU32;
+  pr::DevBuf cside;
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};

@@ -142,13 +142,27 @@ constexpr uint32_t kEntGlobal = 1u << 31;
 constexpr uint32_t kEntZero = 0u;  // LDS slot 0
 constexpr uint32_t kMetaStep0 = 1u << 8;
 constexpr int kMetaExclShift = 14;
-// LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part),
+// Compact entry codes (one part, P = 1; round 3): the codes above cost 4 B per in-link, the
+// largest stream of the pass (4.3 GB at R-MAT s26).  At P = 1 every source of a class-x in-link
+// lies in the class's region of the slice, [x*Q_pad, (x+1)*Q_pad), and its hot set is the first
+// q_load positions of that region, so an entry needs only its region index idx = offset + 1
+// (0 = padding, read as 0.0; hot iff idx <= q_load, LDS slot idx).  Per lane group of 8 entries:
+//   code16[8]  u16: the low 16 bits of idx (one 16-byte load per lane)
+//   side       u32: bits 0-7 the segment-end marks of the 8 entries, bits 8 + 3j .. 10 + 3j the
+//              high 3 bits of entry j's idx (one 4-byte load per lane)
+// -> 2.5 B per in-link, idx < 2^19 (R-MAT s26: Q_pad = 512640).  Larger class regions, and parts
+// of a row partition (whose class sources span several received runs), keep the 32-bit codes.
+constexpr int kCodeU32 = 0;
+constexpr int kCodeC20 = 1;
+constexpr int kC20IdxBits = 19;
+// LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part), one
+// more 0.0 slot (where compact cold entries point their LDS read), the workgroup's unit counter,
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
 // ~0.5 % and 64 by ~0.8 % at R-MAT s26, profiles/r01/stage_ab/).
 constexpr int kStageSlots = 128;
 constexpr int kHotLdsBytes = 160 * 1024;
-constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 2;
-constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18430 hot contributions (144 KiB)
+constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 3;
+constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18429 hot contributions (144 KiB)
 
 // Geometry of the split layout of one part, passed to kernels by value.
 struct ClassGeom {
@@ -171,9 +185,11 @@ struct HotGeom {
   int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;
   __host__ __device__ int slots() const { return P * Kp + 1; }
-  // slot `slots()` is a control word (the workgroup's unit counter, pr_spmv.h hot_class_units);
-  // the staging windows start 16-byte aligned after it
-  __host__ __device__ int stage_off() const { return (slots() + 2) & ~1; }
+  // slot `slots()` holds 0.0 (compact codes' cold entries read it), slot `slots() + 1` is a
+  // control word (the workgroup's unit counter, pr_spmv.h hot_class_units); the staging windows
+  // start 16-byte aligned after it
+  __host__ __device__ int ctr_slot() const { return slots() + 1; }
+  __host__ __device__ int stage_off() const { return (slots() + 3) & ~1; }
   __host__ __device__ size_t lds_bytes() const {
     return sizeof(double) * ((size_t)stage_off() + (size_t)(kHotThreads / 64) * kStageSlots);
   }

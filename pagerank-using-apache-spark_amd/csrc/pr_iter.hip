@@ -159,8 +159,9 @@ int prepare_hot_kernel() {
         PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
-  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_spmv_hot), hipFuncAttributeMaxDynamicSharedMemorySize,
-                             kHotLdsBytes));
+  for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>)})
+    PR_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   return PR_OK;
 }
 
@@ -224,10 +225,12 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
 
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   if (ph1 < 0) ph1 = n_hot_phases(g);
-  hipLaunchKernelGGL(k_spmv_hot, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
-                     g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, g->colh.as<uint32_t>(),
-                     g->cbuf[in].as<double>(), (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(),
-                     g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
+  const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
+  auto kern = g->code == kCodeC20 ? k_spmv_hot<kCodeC20> : k_spmv_hot<kCodeU32>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
+                     g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
+                     (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),
+                     g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }

@@ -302,14 +302,40 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint32_t *_
   }
 }
 
-// The lane metadata of a STREAM unit (pr_internal.h) from the end marks in bit 0 of its codes:
-// which of the lane's entries end a segment, the six "add the partner" predicates of the wave's
-// segmented scan (the partner lanes up to this one hold no segment end), and the index of the
-// lane's first segment end within the unit (an exclusive scan of the per-lane end counts).
-__device__ __forceinline__ uint32_t derive_meta(const WaveCodes &w) {
+// Compact codes (pr_internal.h kCodeC20): lane l's 8 low-index halves (one 16-byte load) and its
+// side word of end marks and high bits (one 4-byte load); lanes past the unit read 0 (padding).
+struct WaveCodesC20 {
+  uint32_t w[kWavePT / 2];
+  uint32_t s;
+};
+__device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint16_t *__restrict__ code16,
+                                                const uint32_t *__restrict__ cside, WaveCodesC20 &w) {
+  const __amdgpu_buffer_rsrc_t rm =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(code16 + (int64_t)u.p8 * 8), 0, u.n * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsd =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(cside + (int64_t)u.p8), 0, u.n / 2, 0x00020000);
+  const pr_v4i x = __builtin_bit_cast(pr_v4i, __builtin_amdgcn_raw_buffer_load_b128(rm, lane_id() * 16, 0, 2));
+  w.w[0] = (uint32_t)x.x;
+  w.w[1] = (uint32_t)x.y;
+  w.w[2] = (uint32_t)x.z;
+  w.w[3] = (uint32_t)x.w;
+  w.s = __builtin_amdgcn_raw_buffer_load_b32(rsd, lane_id() * 4, 0, 2);
+}
+
+// Which of the lane's entries end a segment (bit j: entry j).
+__device__ __forceinline__ uint32_t end_marks(const WaveCodes &w) {
   uint32_t endm = 0;
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) endm |= (w.c[j] & 1u) << j;
+  return endm;
+}
+__device__ __forceinline__ uint32_t end_marks(const WaveCodesC20 &w) { return w.s & 0xFFu; }
+
+// The lane metadata of a STREAM unit (pr_internal.h) from the end marks of its entries: which of
+// the lane's entries end a segment, the six "add the partner" predicates of the wave's segmented
+// scan (the partner lanes up to this one hold no segment end), and the index of the lane's first
+// segment end within the unit (an exclusive scan of the per-lane end counts).
+__device__ __forceinline__ uint32_t derive_meta(uint32_t endm) {
   const int t = lane_id(), r = t & 15, row = t >> 4;
   const uint64_t F = __ballot(endm != 0u);
   const uint64_t upto = (t == 63) ? ~0ull : ((1ull << (t + 1)) - 1);  // lanes [0, t]
@@ -327,17 +353,39 @@ __device__ __forceinline__ uint32_t derive_meta(const WaveCodes &w) {
   return endm | (cond * kMetaStep0) | (excl << kMetaExclShift);
 }
 
+// The gather-space side of a class: 32-bit codes hold byte offsets into the whole gather space;
+// compact codes hold region indices, so class x's descriptor starts past its hot positions
+// (go = 8 idx - hb: hot and padding entries wrap to >= 2^31, out of range) and a cold entry's LDS
+// read is clamped to the 0.0 slot at zb = 8 slots().
+struct ClassSrc {
+  __amdgpu_buffer_rsrc_t crs;
+  uint32_t zb, hb;
+};
+
 // The unit's values: per entry an LDS read (hot) and a range-checked gather-space load (cold),
 // one of them an exact 0.
-__device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, __amdgpu_buffer_rsrc_t crs,
+__device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, const ClassSrc &cs,
                                                  double (&v)[kWavePT]) {
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) {
-    const uint32_t c = w.c[j] & ~1u;  // bit 0: segment end mark (derive_meta)
+    const uint32_t c = w.c[j] & ~1u;  // bit 0: segment end mark (end_marks)
     const uint32_t la = (int32_t)c < 0 ? 0u : c;
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
     const uint32_t go = c ^ kEntGlobal;  // LDS codes become offsets >= 2^31: out of range, no request
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(crs, go, 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, go, 0, 0));
+    v[j] = __dadd_rn(a, b);
+  }
+}
+__device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const double *hot, const ClassSrc &cs,
+                                                 double (&v)[kWavePT]) {
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) {
+    const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
+    const uint32_t idx = lo | (((w.s >> (8 + 3 * j)) & 7u) << 16);
+    const uint32_t b8 = idx << 3;
+    const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
+    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, b8 - cs.hb, 0, 0));
     v[j] = __dadd_rn(a, b);
   }
 }
@@ -388,7 +436,8 @@ __device__ __forceinline__ void stage_segment_sums(uint32_t meta, const double (
   }
 }
 
-__device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes &w, const double (&v)[kWavePT],
+template <class WC>
+__device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, const double (&v)[kWavePT],
                                                  __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
                                                  double *stage) {
   if (u.meta < 0) {  // PIECE of a long segment
@@ -399,7 +448,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
     if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
-  const uint32_t meta = derive_meta(w);
+  const uint32_t meta = derive_meta(end_marks(w));
   double sv[kWavePT], carry;
   wave_segmented_sums(meta, v, sv, &carry);
   // the sums are staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced
@@ -423,6 +472,25 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
   }
 }
 
+// The code streams of a part (pr_internal.h): 32-bit codes, or compact low halves + side words.
+struct CodeSrc {
+  const void *codes;
+  const uint32_t *side;
+};
+template <int CODE>
+struct CodeOf {
+  using T = WaveCodes;
+};
+template <>
+struct CodeOf<kCodeC20> {
+  using T = WaveCodesC20;
+};
+template <int CODE>
+__device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typename CodeOf<CODE>::T &w) {
+  if constexpr (CODE == kCodeC20) wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), cd.side, w);
+  else wave_unit_codes(u, static_cast<const uint32_t *>(cd.codes), w);
+}
+
 // One class's wave units with the class's hot set already in LDS.  The class's unit list is
 // dealt to the XCD's `nteams` workgroups in slices of kWaves consecutive units every
 // nteams * kWaves (this one is `team`; the slice rotates with the phase, so a workgroup on a
@@ -430,12 +498,12 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WaveCodes 
 // take its units in order from a counter in a spare LDS word (zeroed before the class), so a slow
 // wave takes fewer and the waves reach the class's end together (-3.5 % at s26 against a static
 // interleave, profiles/r02/assign_lds_ab/).
+template <int CODE>
 __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, const Unit *__restrict__ units,
                                                 const int64_t *__restrict__ ucum, const HotGeom &hg,
-                                                const uint32_t *__restrict__ colh, const double *hot,
-                                                __amdgpu_buffer_rsrc_t crs, double *__restrict__ partial,
-                                                const int64_t *__restrict__ poff, double *__restrict__ piece_part,
-                                                double *stage) {
+                                                const CodeSrc &cd, const double *hot, const ClassSrc &cs,
+                                                double *__restrict__ partial, const int64_t *__restrict__ poff,
+                                                double *__restrict__ piece_part, double *stage) {
   const int64_t p0 = poff[x];
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc((void *)(partial + p0), 0, (uint32_t)((poff[x + 1] - p0) * 8), 0x00020000);
@@ -443,7 +511,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   constexpr int kWaves = kHotThreads / kWave;
   team = (team + 5 * (x / kXcds)) % nteams;
   const int64_t stride = (int64_t)nteams * kWaves;
-  uint32_t *ctr = reinterpret_cast<uint32_t *>(const_cast<double *>(hot) + hg.slots());
+  uint32_t *ctr = reinterpret_cast<uint32_t *>(const_cast<double *>(hot) + hg.ctr_slot());
   const int lane = lane_id();
   auto take = [&]() -> int64_t {
     uint32_t t = 0;
@@ -462,25 +530,25 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   const int64_t none_k = ucum[kMaxClasses];
   // ring of three units: codes of i+2 in flight while unit i is reduced, then unit i+1's gathers
   Unit u[3];
-  WaveCodes wc[3];
+  typename CodeOf<CODE>::T wc[3];
   double v[3][kWavePT];
   int64_t k1 = take();
   u[0] = unit_at(k);
-  wave_unit_codes(u[0], colh, wc[0]);
+  unit_codes<CODE>(u[0], cd, wc[0]);
   u[1] = unit_at(k1 < end ? k1 : none_k);
-  wave_unit_codes(u[1], colh, wc[1]);
-  wave_unit_gather(wc[0], hot, crs, v[0]);
+  unit_codes<CODE>(u[1], cd, wc[1]);
+  wave_unit_gather(wc[0], hot, cs, v[0]);
   while (true) {
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl) {
       const int s1 = (sl + 1) % 3, s2 = (sl + 2) % 3;
       const int64_t k2 = take();
       u[s2] = unit_at(k2 < end ? k2 : none_k);
-      wave_unit_codes(u[s2], colh, wc[s2]);
+      unit_codes<CODE>(u[s2], cd, wc[s2]);
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/)
       wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
-      wave_unit_gather(wc[s1], hot, crs, v[s1]);
+      wave_unit_gather(wc[s1], hot, cs, v[s1]);
       k = k1;
       k1 = k2;
       if (k >= end) return;
@@ -491,29 +559,38 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
 // The class units of the split layout, one 1024-thread workgroup per CU (a grid that is a
 // multiple of the XCD count).  All of an XCD's workgroups run its classes one after another
 // (phases [ph0, ph1): one launch per phase when the exchange overlaps), restaging the hot set
-// per class.
+// per class.  CODE: the entry code format (pr_internal.h); compact codes address class x's
+// region of the gather space [x*Q_pad, (x+1)*Q_pad) (P = 1 only).
+template <int CODE>
 __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
                                                           const int64_t *__restrict__ ucum, HotGeom hg,
-                                                          const uint32_t *__restrict__ colh,
-                                                          const double *__restrict__ cin, uint32_t cin_bytes,
-                                                          double *__restrict__ partial,
+                                                          CodeSrc cd, const double *__restrict__ cin,
+                                                          uint32_t cin_bytes, double *__restrict__ partial,
                                                           const int64_t *__restrict__ poff,
                                                           double *__restrict__ piece_part,
                                                           const int32_t *__restrict__ hpos, int ph0, int ph1) {
   extern __shared__ double hot[];
   const int nh = hg.P * hg.Kp;
-  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+  ClassSrc cs;
+  cs.zb = (uint32_t)hg.slots() * 8u;
+  cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
+  if constexpr (CODE != kCodeC20) cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int team = (int)(blockIdx.x / kXcds), nteams = (int)(gridDim.x / kXcds);
   for (int ph = ph0; ph < ph1; ++ph) {
     const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
+    if constexpr (CODE == kCodeC20) {  // region index q_load + 1 + k -> position x*Q_pad + q_load + k
+      const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;
+      cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0,
+                                                 (uint32_t)((hg.Q_pad - hg.q_load) * 8), 0x00020000);
+    }
     if (ph > ph0) __syncthreads();  // every wave is done with the previous class's hot set
     // stage the class's hot contributions (the previous iteration's, final before this launch):
     // every position load, then every gather in flight before the first LDS write -- a rolled
     // loop pays two dependent memory latencies per element, 18 times per phase (-2.7 % at s26)
     const int32_t *hp = hpos + (int64_t)x * nh;
-    constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18430 slots)
+    constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18429 slots)
     for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
       int32_t pos[kSB];
       double val[kSB];
@@ -532,10 +609,11 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
     }
     if (threadIdx.x == 0) {
       hot[0] = 0.0;
-      *reinterpret_cast<uint32_t *>(hot + hg.slots()) = 0u;  // the workgroup's unit counter
+      hot[hg.slots()] = 0.0;
+      *reinterpret_cast<uint32_t *>(hot + hg.ctr_slot()) = 0u;  // the workgroup's unit counter
     }
     __syncthreads();
-    hot_class_units(x, team, nteams, units, ucum, hg, colh, hot, crs, partial, poff, piece_part, stage);
+    hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
   }
 }
 

@@ -69,7 +69,7 @@ class PageRankGraph:
         torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (column classes once the
         contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h).  options: build
         options of pr_graph_create_ex by name (_lib.BUILD_OPTIONS: classes, hot_slots,
-        exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow)."""
+        exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow, codes)."""
         L = _lib.load()
         flags = 0
         if dangling == "none":

@@ -560,3 +560,42 @@ def test_epilogue_narrow_workgroups(hip, oracle_c):
             assert np.array_equal(again, out[narrow])
     assert max_rel(out["1"], out["0"]) <= 1e-13
     assert max_rel(out["1"], ref["ranks"]) <= RANK_TOL
+
+
+@pytest.mark.parametrize("classes,slots", [(8, 0), (16, 300), (64, 300), (16, -1), (64, -1)])
+def test_compact_codes_bitwise(hip, oracle_c, classes, slots):
+    """Compact 2.5-byte entry codes (PR_BOPT_CODES default, pr_internal.h kCodeC20): region
+    indices with end marks and high bits in a side word per 8 entries.  Same entries, same sums
+    in the same order as the 32-bit codes, so the ranks are bitwise equal; with no hot set, a
+    partial one and the default one (every class region fully hot here), with hub segments in
+    pieces and empty (row, class) pairs.  Parts of a row partition keep the 32-bit codes."""
+    opts = {"classes": classes, "hot_slots": slots}
+    rng = np.random.default_rng(300 + classes + slots)
+    V = 60000
+    src, dst = random_edges(rng, V, 700000, hub_frac=0.03)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 8, layout="split", options=opts)
+    assert info["code_bits"] == 20 and info["layout"] == 1
+    assert info["n_long_rows"] > 0 or classes > 16  # hub segments in pieces (not at 64 classes)
+    for it in range(8):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+    with hip.PageRankGraph(V, src, dst, layout="split", options=dict(opts, codes=0)) as g:
+        assert g.info()["code_bits"] == 32
+        r32, st32 = g.run(8)
+    assert np.array_equal(r32, ranks)
+    assert [s.dangling_sum for s in st32] == [s.dangling_sum for s in stats]
+    with hip.PageRankGraph(V, src, dst, part=0, n_parts=2, keep_canonical=False, layout="split",
+                           options=opts) as g:
+        assert g.info()["code_bits"] == 32
+
+
+def test_compact_codes_fall_back_for_large_regions(hip, oracle_c):
+    """A class region of 2^19 rows or more does not fit the compact index: 32-bit codes, same
+    ranks as the oracle."""
+    rng = np.random.default_rng(77)
+    V = 4400000  # 8 classes -> Q_pad > 2^19
+    src, dst = random_edges(rng, V, 4000000)
+    csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 4, layout="split",
+                                                  options={"classes": 8})
+    assert info["code_bits"] == 32
+    for it in range(4):
+        assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
