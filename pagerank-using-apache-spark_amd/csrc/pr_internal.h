@@ -131,17 +131,12 @@ constexpr uint32_t kRowHole = 1u << 30;    // padding row of the class layout
 //   bit 31 clear  LDS byte address of a hot-set slot; slot 0 (address 0) holds 0.0
 //   bit 0         set on the last entry of a segment (both kinds are multiples of 8 otherwise)
 // Padding entries are 0 -- also what a range-checked load past the unit returns.  k_spmv_hot
-// derives a per-lane metadata word from the end marks (pr_spmv.h derive_meta):
-//   bits 0-7   which of the lane's entries end a segment (STREAM)
-//   bits 8-13  the six partner-add predicates of the wave's segmented scan (pr_spmv.h)
-//   bits 14-23 segment index of the lane's first end within the unit
+// derives each lane's scan metadata from the end marks (pr_spmv.h derive_meta).
 constexpr int kWavePT = 8;
 constexpr int kWaveUnit = 64 * kWavePT;  // 512 (wave64)
 constexpr int kHotThreads = 1024;        // 16 waves per CU: one workgroup per CU
 constexpr uint32_t kEntGlobal = 1u << 31;
 constexpr uint32_t kEntZero = 0u;  // LDS slot 0
-constexpr uint32_t kMetaStep0 = 1u << 8;
-constexpr int kMetaExclShift = 14;
 // Compact entry codes (one part, P = 1; round 3): the codes above cost 4 B per in-link, the
 // largest stream of the pass (4.3 GB at R-MAT s26).  At P = 1 every source of a class-x in-link
 // lies in the class's region of the slice, [x*Q_pad, (x+1)*Q_pad), and its hot set is the first

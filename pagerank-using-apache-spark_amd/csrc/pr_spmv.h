@@ -282,6 +282,20 @@ __device__ __forceinline__ int wave_incl_scan_i32(int x) {
   return x;
 }
 
+// Inclusive wave64 max-scan of a non-negative int (0 is neutral: what bound_ctrl reads).
+__device__ __forceinline__ int wave_incl_max_i32(int x) {
+  const int row = lane_id() >> 4;
+  x = max(x, dpp_i32<0x111>(x));
+  x = max(x, dpp_i32<0x112>(x));
+  x = max(x, dpp_i32<0x114>(x));
+  x = max(x, dpp_i32<0x118>(x));
+  int p = dpp_i32<0x142>(x);
+  if (row == 1 || row == 3) x = max(x, p);
+  p = dpp_i32<0x143>(x);
+  if (row >= 2) x = max(x, p);
+  return x;
+}
+
 struct WaveCodes {
   uint32_t c[kWavePT];
 };
@@ -331,26 +345,33 @@ __device__ __forceinline__ uint32_t end_marks(const WaveCodes &w) {
 }
 __device__ __forceinline__ uint32_t end_marks(const WaveCodesC20 &w) { return w.s & 0xFFu; }
 
-// The lane metadata of a STREAM unit (pr_internal.h) from the end marks of its entries: which of
-// the lane's entries end a segment, the six "add the partner" predicates of the wave's segmented
-// scan (the partner lanes up to this one hold no segment end), and the index of the lane's first
-// segment end within the unit (an exclusive scan of the per-lane end counts).
-__device__ __forceinline__ uint32_t derive_meta(uint32_t endm) {
+// The lane metadata of a STREAM unit from the end marks of its entries: which of the lane's
+// entries end a segment, the index (within the unit) of the lane's first segment end (an
+// exclusive scan of the per-lane end counts), and the six "add the partner" predicates of the
+// wave's segmented scan (step k: no segment end in the lanes from the partner + 1 to this one).
+// The predicates come from one max-scan: d = distance to the last lane at or before this one
+// that holds an end (t + 1 if none); the row_shr k step needs d >= k (and the partner in the
+// row), row_bcast 15 d > r, row_bcast 31 d > t - 32.  About half the VALU of testing the end
+// ballot per step.
+struct LaneMeta {
+  uint32_t endm;
+  int excl;
+  bool c[6];
+};
+__device__ __forceinline__ LaneMeta derive_meta(uint32_t endm) {
+  LaneMeta m;
+  m.endm = endm;
   const int t = lane_id(), r = t & 15, row = t >> 4;
-  const uint64_t F = __ballot(endm != 0u);
-  const uint64_t upto = (t == 63) ? ~0ull : ((1ull << (t + 1)) - 1);  // lanes [0, t]
-  auto clear = [&](int lo) { return (F & upto & ~((1ull << lo) - 1)) == 0ull; };  // no end in [lo, t]
-  uint32_t cond = 0;
+  const int last1 = wave_incl_max_i32(endm ? t + 1 : 0);  // last lane <= t with an end, + 1 (0: none)
+  const int d = t + 1 - last1;
+  const int dr = min(d, r);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int k = 1 << s;
-    if (r >= k && clear(t - k + 1)) cond |= 1u << s;
-  }
-  if ((row == 1 || row == 3) && clear(row * 16)) cond |= 1u << 4;
-  if (row >= 2 && clear(32)) cond |= 1u << 5;
+  for (int s = 0; s < 4; ++s) m.c[s] = dr >= (1 << s);
+  m.c[4] = (row & 1) && d > r;
+  m.c[5] = row >= 2 && d > t - 32;
   const int cnt = __builtin_popcount(endm);
-  const uint32_t excl = (uint32_t)(wave_incl_scan_i32(cnt) - cnt);
-  return endm | (cond * kMetaStep0) | (excl << kMetaExclShift);
+  m.excl = wave_incl_scan_i32(cnt) - cnt;
+  return m;
 }
 
 // The gather-space side of a class: 32-bit codes hold byte offsets into the whole gather space;
@@ -392,48 +413,47 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
 
 // Per-lane sums along the segment ends, then the wave's segmented scan; on return sv[j] is the
 // lane's running sum at entry j (restarted after every end) and *carry the sum flowing into the
-// lane's first segment from earlier lanes.  meta = derive_meta(w).
-__device__ __forceinline__ void wave_segmented_sums(uint32_t meta, const double (&v)[kWavePT], double (&sv)[kWavePT],
-                                                    double *carry) {
-  const uint32_t endm = meta & 0xFFu;
+// lane's first segment from earlier lanes.
+__device__ __forceinline__ void wave_segmented_sums(const LaneMeta &m, const double (&v)[kWavePT],
+                                                    double (&sv)[kWavePT], double *carry) {
   double acc = 0.0;
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) {
     acc = __dadd_rn(acc, v[j]);
     sv[j] = acc;
-    if (endm & (1u << j)) acc = 0.0;
+    if (m.endm & (1u << j)) acc = 0.0;
   }
-  // segmented inclusive scan of the lane tails; partner-add predicates from the metadata
+  // segmented inclusive scan of the lane tails
   double a = acc, p;
   p = dpp_f64<0x111>(a);  // row_shr:1
-  if (meta & kMetaStep0) a = __dadd_rn(p, a);
+  if (m.c[0]) a = __dadd_rn(p, a);
   p = dpp_f64<0x112>(a);  // row_shr:2
-  if (meta & (kMetaStep0 << 1)) a = __dadd_rn(p, a);
+  if (m.c[1]) a = __dadd_rn(p, a);
   p = dpp_f64<0x114>(a);  // row_shr:4
-  if (meta & (kMetaStep0 << 2)) a = __dadd_rn(p, a);
+  if (m.c[2]) a = __dadd_rn(p, a);
   p = dpp_f64<0x118>(a);  // row_shr:8
-  if (meta & (kMetaStep0 << 3)) a = __dadd_rn(p, a);
+  if (m.c[3]) a = __dadd_rn(p, a);
   p = dpp_f64<0x142>(a);  // row_bcast:15
-  if (meta & (kMetaStep0 << 4)) a = __dadd_rn(p, a);
+  if (m.c[4]) a = __dadd_rn(p, a);
   p = dpp_f64<0x143>(a);  // row_bcast:31
-  if (meta & (kMetaStep0 << 5)) a = __dadd_rn(p, a);
+  if (m.c[5]) a = __dadd_rn(p, a);
   *carry = dpp_f64<0x138>(a);  // wave_shr:1 (lane 0 reads 0)
 }
 
-// Segment sums of staged pass [base, base + kStageSlots) into the wave's LDS window: the lane's
-// first segment end gets the carry.
-__device__ __forceinline__ void stage_segment_sums(uint32_t meta, const double (&sv)[kWavePT], double carry, int base,
-                                                   double *stage) {
-  const uint32_t endm = meta & 0xFFu;
-  int e = (int)(meta >> kMetaExclShift) - base;
-  bool first = true;
+// Segment sums of staged pass [base, base + kStageSlots) into the wave's LDS window; the lane's
+// first segment end then gets the carry added in place (carry + its sum: the same add as before
+// staging, one add per lane instead of a speculative one per entry).
+__device__ __forceinline__ void stage_segment_sums(const LaneMeta &m, const double (&sv)[kWavePT], double carry,
+                                                   int base, double *stage) {
+  int e = m.excl - base;
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) {
-    const bool end = (endm >> j) & 1u;
-    if (end && e >= 0 && e < kStageSlots) stage[e] = first ? __dadd_rn(carry, sv[j]) : sv[j];
-    if (end) first = false;
+    const bool end = (m.endm >> j) & 1u;
+    if (end && e >= 0 && e < kStageSlots) stage[e] = sv[j];
     e += end ? 1 : 0;
   }
+  const int e0 = m.excl - base;
+  if (m.endm != 0u && e0 >= 0 && e0 < kStageSlots) stage[e0] = __dadd_rn(carry, stage[e0]);
 }
 
 template <class WC>
@@ -448,9 +468,9 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, con
     if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
     return;
   }
-  const uint32_t meta = derive_meta(end_marks(w));
+  const LaneMeta m = derive_meta(end_marks(w));
   double sv[kWavePT], carry;
-  wave_segmented_sums(meta, v, sv, &carry);
+  wave_segmented_sums(m, v, sv, &carry);
   // the sums are staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced
   // stores: two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an
   // odd last slot alone -- half the store instructions of one 8-byte store per slot (-1.7 % at
@@ -459,7 +479,7 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, con
   const int nseg = u.meta;
   static_assert(kStageSlots <= 2 * kWave, "one b128 pass");
   for (int base = 0; base < nseg; base += kStageSlots) {
-    stage_segment_sums(meta, sv, carry, base, stage);
+    stage_segment_sums(m, sv, carry, base, stage);
     const int n = min(kStageSlots, nseg - base);
     const int i2 = 2 * lane_id();
     const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
