@@ -192,6 +192,11 @@ def main() -> int:
                     help="deadline of every stage in seconds (default: per stage, 180-900 s)")
     ap.add_argument("--simulate-stall", choices=STAGES, default=None,
                     help="test hook: hang in this stage (before any GPU work) to exercise the watchdog")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal of the N > 1 path on a box with fewer GPUs than ranks: rank r runs on "
+                         "device r %% count and poses to RCCL as a host of its own (NCCL_HOSTID), so RCCL's "
+                         "duplicate-GPU check passes and the ranks talk over its socket transport on "
+                         "loopback -- the library's RCCL exchange executes for real; its speed means nothing")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -215,6 +220,11 @@ def main() -> int:
     if world != a.gpus:
         log(f"WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
     dev = local_rank
+    if a.share_device and world > 1:
+        # before torch's process group and the library create their RCCL communicators
+        dev = local_rank % max(torch.cuda.device_count(), 1)
+        os.environ["NCCL_HOSTID"] = f"pr-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     wd.enter("init", limits["init"])
     torch.cuda.set_device(dev)
     dist = None
@@ -421,6 +431,8 @@ def main() -> int:
                 "build_options": bopts or None,
                 "layout": ["fused", "split"][info.get("layout", 0)],
                 "hot_cover": round(info.get("hot_cover_ppm", 0) / 1e6, 4),
+                # --share-device: a correctness rehearsal (ranks share GPUs, RCCL over loopback sockets)
+                "shared_device_rehearsal": bool(a.share_device and world > 1),
             },
             "roofline": {
                 "bound": "hbm",

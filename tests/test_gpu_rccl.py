@@ -1,0 +1,71 @@
+"""The RCCL transport of the row-partitioned iteration, executed on a one-GPU box.
+
+The multi-GPU path (one process per GPU, per-peer ncclSend/ncclRecv of the contributions each part
+reads, Sparky.java:192's re-shuffle) normally needs as many GPUs as ranks, and RCCL refuses two
+ranks on one device ("Duplicate GPU detected").  `bench.py --share-device` runs every rank on
+GPU 0 and gives each rank its own NCCL_HOSTID, so RCCL treats the ranks as separate hosts and
+connects them through its socket transport on loopback: the library's communicator attach, its
+exchange agreement check (ncclAllGather of the run records), the grouped send/recv of the
+unchunked and chunked exchange and torch's process group around them all execute for real.
+The bench then checks every rank's rows, summed on rank 0, against the oracle (Sparky.java:233 after
+10 iterations) for both exchange modes.  Throughput of such a run means nothing.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RANK_TOL = 1e-9
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, extra, scale=20, timeout=280):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--share-device", "--scale", str(scale), "--steps", "6", "--warmup", "2",
+           "--parity-iters", "10", "--stage-timeout", "150"] + extra
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert p.returncode == 0 and lines, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-5000:]}"
+    line = json.loads(lines[-1])
+    print(f"world {world} {extra}: exchange {line['config']['exchange_mode']} "
+          f"doubles/iter rank0 {line['config']['exchange_doubles_per_iter_rank0']} "
+          f"overlap_ab {line['exchange_overlap_ab']} parity {line['parity']}")
+    return line
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(320)
+@pytest.mark.parametrize(
+    "world,extra",
+    [
+        (2, ["--build-option", "classes=16"]),  # sparse runs; calibration of unchunked / chunked (2 chunks)
+        (3, ["--build-option", "classes=32"]),  # odd rank count, 4 chunks per run
+        (2, ["--build-option", "exchange_allgather=1"]),  # whole-slice ncclAllGather (A/B reference)
+    ],
+    ids=["p2-c16-sparse", "p3-c32-sparse", "p2-allgather"],
+)
+def test_rccl_exchange_on_shared_device(world, extra):
+    line = _run(world, extra)
+    assert line["n_gpus"] == world
+    assert line["config"]["shared_device_rehearsal"] is True
+    par = line["parity"]
+    assert par is not None and par["ranks_from"] == f"{world} rank(s)"
+    assert par["every_row_owned_once"] is True
+    assert par["max_rel"] <= RANK_TOL
+    if "exchange_allgather=1" not in extra:
+        assert line["config"]["exchange_doubles_per_iter_rank0"] > 0
+        ab = line["exchange_overlap_ab"]
+        assert ab is not None and ab["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1",
+                                                   "chunked_reserve2")
+        assert par["max_rel_overlapped_exchange"] <= RANK_TOL

@@ -58,6 +58,39 @@ __global__ __launch_bounds__(256) void k_ta_probe(const double *__restrict__ tab
   }
   if (acc == 12345.0) out[t] = acc;
 }
+// Stream probe: every thread issues 8 coalesced buffer loads (or stores) of W bytes per lane; a
+// wave's lanes cover one contiguous 64 W-byte run per instruction, the table wrapping (2 MiB: L2
+// resident; 1 GiB: HBM).  Lanes >= active are exec-masked.  Time per instruction vs W and active
+// lanes gives the vector-memory path's cost of the code loads and partial-slot stores of
+// k_spmv_hot (one b128 + one b32 load and ~1 b128 store per wave unit).
+typedef unsigned int prd_u32x2 __attribute__((__vector_size__(8)));
+typedef unsigned int prd_u32x4 __attribute__((__vector_size__(16)));
+template <int W, bool STORE>
+__global__ __launch_bounds__(256) void k_stream_probe(char *__restrict__ table, uint32_t table_bytes, int64_t n_threads,
+                                                      int active, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_threads) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, table_bytes, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)(t >> 6);
+  uint32_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t off = (uint32_t)((((wave * 8 + j) * 64 + lane) * W) % table_bytes);
+    if (lane < active) {
+      if constexpr (STORE) {
+        if constexpr (W == 4) __builtin_amdgcn_raw_buffer_store_b32(lane + j, rs, off, 0, 0);
+        else if constexpr (W == 8) __builtin_amdgcn_raw_buffer_store_b64(prd_u32x2{(unsigned)lane, (unsigned)j}, rs, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(prd_u32x4{(unsigned)lane, (unsigned)j, 1u, 2u}, rs, off, 0, 0);
+      } else {
+        if constexpr (W == 4) acc ^= __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        else if constexpr (W == 8) { const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0); acc ^= v[0] ^ v[1]; }
+        else { const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0); acc ^= v[0] ^ v[1] ^ v[2] ^ v[3]; }
+      }
+    }
+  }
+  if (acc == 12345u) out[t] = acc;
+}
 // CU-mask probe: every workgroup (one wave) records its XCC id and raw HW_ID register (CU, SH, SE
 // fields), so a stream's CU-mask bits can be mapped to physical CUs and XCDs.
 __global__ void k_cu_probe(uint32_t *__restrict__ out) {
@@ -150,6 +183,50 @@ int prd_ta_probe(int device, int64_t table_bytes, int64_t n_loads, int active, i
     for (int i = 0; i < (rep ? iters : 1); ++i) {
       if (masked) hipLaunchKernelGGL(k_ta_probe<true>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
       else hipLaunchKernelGGL(k_ta_probe<false>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
+    }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
+  return 0;
+}
+
+// Stream probe (see k_stream_probe): width 4 / 8 / 16 bytes per lane, store 0/1; n_instr = 8 *
+// threads / 64 wave instructions; returns ms per launch.
+int prd_stream_probe(int device, int64_t table_bytes, int64_t n_loads, int width, int store, int active, int iters,
+                     double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  void *tab = nullptr, *out = nullptr;
+  PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8));
+  const int64_t nt = n_loads / 8;
+  const dim3 grid((unsigned)((nt + 255) / 256));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i) {
+      char *T = (char *)tab;
+      const uint32_t tb = (uint32_t)table_bytes;
+      double *O = (double *)out;
+      if (store) {
+        if (width == 4) hipLaunchKernelGGL((k_stream_probe<4, true>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+        else if (width == 8) hipLaunchKernelGGL((k_stream_probe<8, true>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+        else hipLaunchKernelGGL((k_stream_probe<16, true>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+      } else {
+        if (width == 4) hipLaunchKernelGGL((k_stream_probe<4, false>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+        else if (width == 8) hipLaunchKernelGGL((k_stream_probe<8, false>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+        else hipLaunchKernelGGL((k_stream_probe<16, false>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
+      }
     }
     PR_HIP(hipGetLastError());
     PR_HIP(hipEventRecord(b, 0));

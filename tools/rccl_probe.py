@@ -4,7 +4,9 @@ iterations, and rank 0 checks the merged ranks against the single-part run.
 
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 tools/rccl_probe.py [--exchange sparse|allgather]
-RCCL may refuse two ranks on one device; the probe then reports that and exits 3.
+RCCL refuses two ranks on one device ("Duplicate GPU detected") unless every rank poses as a
+host of its own: the probe sets NCCL_HOSTID per rank (and NCCL_SOCKET_IFNAME=lo), so the ranks
+connect through RCCL's socket transport on loopback (bench.py --share-device does the same).
 """
 import argparse
 import os
@@ -27,6 +29,8 @@ def main():
     a = ap.parse_args()
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
+    os.environ["NCCL_HOSTID"] = f"pr-probe-rank{rank}"  # before any RCCL call in this process
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     E = 16 << a.scale
