@@ -27,6 +27,10 @@ typedef struct prh_edges prh_edges;
 
 const char *prh_last_error(void);
 int prh_read(const char *path, int32_t format, prh_edges **out);
+/* Threads of the edge-list reader (PRH_FORMAT_EDGES): 0 = automatic (one for inputs under 16 MiB,
+   else the host's granted cores, at most 64).  The IDs are the same for any count: first
+   appearance in file order, src before dst. */
+void prh_set_read_threads(int32_t n);
 /* the same from a memory buffer (tests, embedding) */
 int prh_parse(const char *data, int64_t len, int32_t format, prh_edges **out);
 int64_t prh_n_edges(const prh_edges *e);

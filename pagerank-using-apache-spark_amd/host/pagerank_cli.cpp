@@ -161,14 +161,20 @@ int run_group(const Options &o, const prh_edges *edges, const double *init, int 
 
 }  // namespace
 
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
 int main(int argc, char **argv) {
   const Options o = parse(argc, argv);
+  const auto t_job = Clock::now();
   prh_edges *edges = nullptr;
   if (prh_read(o.path.c_str(), o.format, &edges) != 0) {
     std::fprintf(stderr, "pagerank: %s\n", prh_last_error());
     return 1;
   }
   const int32_t V = prh_n_vertices(edges);
+  const double ms_read = ms_since(t_job);  // parse + first-appearance interning (host)
+  double ms_build = 0.0, ms_run = 0.0;
   Job job{&o, edges};
   std::vector<double> ranks((size_t)V + 1), init;
   if (!o.resume.empty()) {
@@ -184,21 +190,27 @@ int main(int argc, char **argv) {
   const double *init_p = init.empty() ? nullptr : init.data();
   if (o.devices.size() > 1) {
     if (n_run > 0) std::printf("Starting iter%d\n", job.start);
+    const auto t0 = Clock::now();
     if (run_group(o, edges, init_p, n_run, &job, &ranks) != PR_OK) {
       prh_free(edges);
       return 1;
     }
+    ms_run = ms_since(t0);  // group: build + iterations
   } else {
     const int dev = o.devices.empty() ? o.device : o.devices[0];
     pr_graph *g = nullptr;
+    auto t0 = Clock::now();
     int rc = pr_graph_create(dev, V, prh_n_edges(edges), prh_src(edges), prh_dst(edges), o.flags | PR_NO_CANONICAL, &g);
+    ms_build = ms_since(t0);
     if (rc != PR_OK) {
       std::fprintf(stderr, "pagerank: graph build failed (%d): %s\n", rc, pr_last_error());
       prh_free(edges);
       return 1;
     }
     if (n_run > 0) std::printf("Starting iter%d\n", job.start);
+    t0 = Clock::now();
     rc = pr_run(g, n_run, 0.15, 0.85, init_p, ranks.data(), on_iter, o.out.empty() ? 0u : PR_CB_RANKS, &job);
+    ms_run = ms_since(t0);  // iterations, with the per-iteration callback (and its part-file writes)
     pr_graph_destroy(g);
     if (rc != PR_OK) {
       std::fprintf(stderr, "pagerank: run failed (%d): %s\n", rc, pr_last_error());
@@ -207,10 +219,18 @@ int main(int argc, char **argv) {
     }
   }
   std::fflush(stdout);
+  const auto t_out = Clock::now();
   if (!o.quiet && prh_write_has_rank(edges, nullptr, ranks.data()) != 0) {
     std::fprintf(stderr, "pagerank: %s\n", prh_last_error());
     job.error = 1;
   }
+  std::fflush(stdout);
+  const double ms_out = ms_since(t_out);
+  if (o.stats)  // the job's phases (wall clock); one JSON object on stderr
+    std::fprintf(stderr,
+                 "{\"job\": {\"urls\": %d, \"edge_records\": %lld, \"read_intern_ms\": %.1f, \"build_ms\": %.1f, "
+                 "\"iterations\": %d, \"run_ms\": %.1f, \"has_rank_out_ms\": %.1f, \"total_ms\": %.1f}}\n",
+                 V, (long long)prh_n_edges(edges), ms_read, ms_build, n_run, ms_run, ms_out, ms_since(t_job));
   prh_free(edges);
   return job.error;
 }

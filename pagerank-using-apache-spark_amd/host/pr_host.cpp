@@ -9,6 +9,8 @@
 
 #include <dirent.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cerrno>
 #include <cmath>
@@ -20,6 +22,7 @@
 #include <memory>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -37,28 +40,61 @@ int fail(const std::string &m) {
 // ---- first-appearance interner over string_views (storage owned elsewhere) ----------------
 class Interner {
  public:
-  explicit Interner(size_t expect) { rehash(expect < 1024 ? 2048 : next_pow2(expect * 2)); }
-  int32_t intern(std::string_view s) {
-    const uint64_t h = hash(s);
+  // expect: a guess of the distinct names; the table starts at most 2^17 slots and doubles as it
+  // fills (a table sized for the input bytes would be mostly empty and miss the caches / TLB on
+  // every probe: an edge list names each URL many times)
+  explicit Interner(size_t expect) { rehash(next_pow2(std::min<size_t>(std::max<size_t>(expect * 2, 2048), 1 << 17))); }
+  int32_t intern(std::string_view s) { return intern_hashed(s, hash(s)); }
+  int32_t intern_hashed(std::string_view s, uint64_t h) {
     size_t i = h & mask_;
     while (true) {
       Slot &sl = slots_[i];
       if (sl.id < 0) {
         sl.id = (int32_t)names_.size();
         sl.hash = h;
+        sl.p = s.data();
+        sl.len = (uint32_t)s.size();
         names_.push_back(s);
+        hashes_.push_back(h);
         if (names_.size() * 2 > slots_.size()) rehash(slots_.size() * 2);
         return (int32_t)names_.size() - 1;
       }
-      if (sl.hash == h && names_[sl.id] == s) return sl.id;
+      if (sl.hash == h && sl.len == s.size() && std::memcmp(sl.p, s.data(), s.size()) == 0) return sl.id;
       i = (i + 1) & mask_;
     }
   }
+  // software prefetch of a probe's first slot, then of the name it holds (batched readers)
+  void prefetch_slot(uint64_t h) const { __builtin_prefetch(&slots_[h & mask_]); }
+  void prefetch_name(uint64_t h) const {
+    const Slot &sl = slots_[h & mask_];
+    if (sl.id >= 0) __builtin_prefetch(sl.p);
+  }
   std::vector<std::string_view> &names() { return names_; }
+  const std::vector<uint64_t> &hashes() const { return hashes_; }
+  // 8 bytes per step (multiply-xorshift), the tail bytes packed into one word, murmur finaliser
+  static uint64_t hash(std::string_view s) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)s.size();
+    const char *p = s.data();
+    size_t n = s.size();
+    for (; n >= 8; n -= 8, p += 8) {
+      uint64_t w;
+      std::memcpy(&w, p, 8);
+      h = (h ^ w) * 0xff51afd7ed558ccdull;
+      h ^= h >> 29;
+    }
+    uint64_t t = 0;
+    for (size_t k = 0; k < n; ++k) t |= (uint64_t)(unsigned char)p[k] << (8 * k);
+    h = (h ^ t) * 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    return h ^ (h >> 33);
+  }
 
  private:
-  struct Slot {
+  struct Slot {  // the name's bytes are compared in place (one memory access per hit)
     uint64_t hash;
+    const char *p;
+    uint32_t len;
     int32_t id;
   };
   static size_t next_pow2(size_t x) {
@@ -66,17 +102,10 @@ class Interner {
     while (p < x) p <<= 1;
     return p;
   }
-  static uint64_t hash(std::string_view s) {  // FNV-1a 64 + murmur finaliser
-    uint64_t h = 1469598103934665603ull;
-    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
-    h ^= h >> 33;
-    h *= 0xff51afd7ed558ccdull;
-    return h ^ (h >> 33);
-  }
   void rehash(size_t n) {
     std::vector<Slot> old;
     old.swap(slots_);
-    slots_.assign(n, Slot{0, -1});
+    slots_.assign(n, Slot{0, nullptr, 0, -1});
     mask_ = n - 1;
     for (const Slot &sl : old) {
       if (sl.id < 0) continue;
@@ -87,6 +116,7 @@ class Interner {
   }
   std::vector<Slot> slots_;
   std::vector<std::string_view> names_;
+  std::vector<uint64_t> hashes_;
   size_t mask_ = 0;
 };
 
@@ -470,7 +500,177 @@ int extract_links(std::string_view url, const char *jb, const char *je, prh_edge
   return 0;
 }
 
+// Tokens of one edge-list line [b, e) (space / tab separated): returns how many there are, the
+// first two in tok.
+int edge_tokens(const char *data, size_t b, size_t e, std::string_view (&tok)[2]) {
+  int nt = 0;
+  size_t j = b;
+  while (j < e) {
+    while (j < e && (data[j] == ' ' || data[j] == '\t')) ++j;
+    if (j >= e) break;
+    const size_t tb = j;
+    while (j < e && data[j] != ' ' && data[j] != '\t') ++j;
+    if (nt < 2) tok[nt] = std::string_view(data + tb, j - tb);
+    ++nt;
+  }
+  return nt;
+}
+
+std::string too_many_tokens(size_t lineno, int nt) {
+  return "line " + std::to_string(lineno) + ": expected 'src [dst]', got " + std::to_string(nt) + " tokens";
+}
+
+int g_read_threads = 0;  // prh_set_read_threads; 0: automatic
+
+// Host threads for the edge-list reader: the affinity mask, capped by the cgroup CPU quota (a GPU
+// box shows the whole machine but grants a share of it) and 64.
+int host_threads() {
+  int n = (int)std::thread::hardware_concurrency();
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0) n = CPU_COUNT(&cs);
+  if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0)
+      n = std::min(n, (int)std::max(1LL, (std::atoll(q) + period - 1) / period));
+    std::fclose(f);
+  }
+  return std::max(1, std::min(n, 64));
+}
+
+// One chunk of an edge list (whole lines) interned on its own: local IDs in first-appearance order
+// within the chunk.
+struct EdgeChunk {
+  size_t b = 0, e = 0;
+  size_t lines = 0;      // records seen ('\n'-terminated, and a last unterminated one)
+  size_t bad_line = 0;   // 1-based line (within the chunk) of the first malformed record, 0: none
+  int bad_tokens = 0;
+  std::vector<int32_t> src, dst;
+  std::unique_ptr<Interner> in;
+};
+
+void parse_edge_chunk(const char *data, EdgeChunk &c) {
+  c.in.reset(new Interner((c.e - c.b) / 32));
+  Interner &in = *c.in;
+  // lines in batches: tokenize and hash a batch, prefetch every token's first slot and then the
+  // name it holds, then intern in line order (the same IDs as one token at a time)
+  constexpr int kB = 32;
+  std::string_view tok[kB][2];
+  uint64_t h[kB][2];
+  int nt[kB];
+  size_t i = c.b;
+  while (i < c.e) {
+    int nb = 0;
+    while (nb < kB && i < c.e) {
+      ++c.lines;
+      const size_t b = i;
+      const char *nl = static_cast<const char *>(std::memchr(data + i, '\n', c.e - i));
+      size_t e = nl ? (size_t)(nl - data) : c.e;
+      i = e + 1;
+      if (e > b && data[e - 1] == '\r') --e;
+      const int n = edge_tokens(data, b, e, tok[nb]);
+      if (n == 0) continue;
+      if (n > 2) {  // the lines before it in this batch are still interned, as sequentially
+        c.bad_line = c.lines;
+        c.bad_tokens = n;
+        break;
+      }
+      nt[nb++] = n;
+    }
+    for (int k = 0; k < nb; ++k)
+      for (int j = 0; j < nt[k]; ++j) in.prefetch_slot(h[k][j] = Interner::hash(tok[k][j]));
+    for (int k = 0; k < nb; ++k)
+      for (int j = 0; j < nt[k]; ++j) in.prefetch_name(h[k][j]);
+    for (int k = 0; k < nb; ++k) {
+      c.src.push_back(in.intern_hashed(tok[k][0], h[k][0]));
+      c.dst.push_back(nt[k] == 2 ? in.intern_hashed(tok[k][1], h[k][1]) : -1);
+    }
+    if (c.bad_line) return;
+  }
+}
+
+// Edge list on T threads, IDs exactly those of the sequential reader (first appearance in file
+// order, src before dst): every chunk interns its lines locally in parallel; then the chunks' local
+// name lists are merged in chunk order into the global interner (a name new to chunk c gets its ID
+// in c's local order, which is file order), and the local IDs are translated in parallel.
+int parse_edges_parallel(const char *data, size_t n, int T, prh_edges *E) {
+  std::vector<size_t> starts{0};
+  for (int t = 1; t < T; ++t) {
+    const size_t p = n * (size_t)t / (size_t)T;
+    if (p == 0) continue;
+    const char *nl = static_cast<const char *>(std::memchr(data + p - 1, '\n', n - (p - 1)));
+    const size_t st = nl ? (size_t)(nl - data) + 1 : n;
+    if (st < n && st > starts.back()) starts.push_back(st);
+  }
+  const size_t C = starts.size();
+  std::vector<EdgeChunk> ch(C);
+  for (size_t c = 0; c < C; ++c) {
+    ch[c].b = starts[c];
+    ch[c].e = c + 1 < C ? starts[c + 1] : n;
+  }
+  {
+    std::vector<std::thread> th;
+    for (size_t c = 0; c < C; ++c) th.emplace_back(parse_edge_chunk, data, std::ref(ch[c]));
+    for (auto &t : th) t.join();
+  }
+  size_t line0 = 0, total = 0, local_names = 0;
+  for (size_t c = 0; c < C; ++c) {
+    if (ch[c].bad_line) return fail(too_many_tokens(line0 + ch[c].bad_line, ch[c].bad_tokens));
+    line0 += ch[c].lines;
+    total += ch[c].src.size();
+    local_names += ch[c].in->names().size();
+  }
+  if (C == 1) {  // one chunk: its local IDs are the IDs
+    E->src.swap(ch[0].src);
+    E->dst.swap(ch[0].dst);
+    E->names.swap(ch[0].in->names());
+    if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
+    return 0;
+  }
+  Interner g(std::max(local_names / 2, (size_t)1024));
+  std::vector<std::vector<int32_t>> to_global(C);
+  for (size_t c = 0; c < C; ++c) {
+    const auto &nm = ch[c].in->names();
+    const auto &hs = ch[c].in->hashes();
+    to_global[c].resize(nm.size());
+    constexpr size_t kB = 32;  // batches with prefetched slots and names, as in parse_edge_chunk
+    for (size_t k0 = 0; k0 < nm.size(); k0 += kB) {
+      const size_t k1 = std::min(nm.size(), k0 + kB);
+      for (size_t k = k0; k < k1; ++k) g.prefetch_slot(hs[k]);
+      for (size_t k = k0; k < k1; ++k) g.prefetch_name(hs[k]);
+      for (size_t k = k0; k < k1; ++k) to_global[c][k] = g.intern_hashed(nm[k], hs[k]);
+    }
+    ch[c].in.reset();  // the views stay valid: they point into the input
+  }
+  E->src.resize(total);
+  E->dst.resize(total);
+  {
+    std::vector<std::thread> th;
+    size_t off = 0;
+    for (size_t c = 0; c < C; ++c) {
+      th.emplace_back([&E, &ch, &to_global, c, off]() {
+        const std::vector<int32_t> &m = to_global[c];
+        const EdgeChunk &k = ch[c];
+        for (size_t i = 0; i < k.src.size(); ++i) {
+          E->src[off + i] = m[k.src[i]];
+          E->dst[off + i] = k.dst[i] < 0 ? -1 : m[k.dst[i]];
+        }
+      });
+      off += ch[c].src.size();
+    }
+    for (auto &t : th) t.join();
+  }
+  E->names.swap(g.names());
+  if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
+  return 0;
+}
+
 int parse_into(const char *data, size_t n, int32_t format, prh_edges *E) {
+  if (format == PRH_FORMAT_EDGES) {
+    // large inputs (or an explicit thread count) on several threads; the same IDs either way
+    const int T = g_read_threads > 0 ? g_read_threads : (n >= ((size_t)16 << 20) ? host_threads() : 1);
+    return parse_edges_parallel(data, n, T, E);
+  }
   Interner in(n / 32);
   size_t i = 0, lineno = 0;
   while (i < n) {
@@ -489,20 +689,10 @@ int parse_into(const char *data, size_t n, int32_t format, prh_edges *E) {
         return -1;
       continue;
     }
-    std::string_view tok[3];
-    int nt = 0;
-    size_t j = b;
-    while (j < e) {
-      while (j < e && (data[j] == ' ' || data[j] == '\t')) ++j;
-      if (j >= e) break;
-      size_t tb = j;
-      while (j < e && data[j] != ' ' && data[j] != '\t') ++j;
-      if (nt < 3) tok[nt] = std::string_view(data + tb, j - tb);
-      ++nt;
-    }
+    std::string_view tok[2];
+    const int nt = edge_tokens(data, b, e, tok);
     if (nt == 0) continue;
-    if (nt > 2)
-      return fail("line " + std::to_string(lineno) + ": expected 'src [dst]', got " + std::to_string(nt) + " tokens");
+    if (nt > 2) return fail(too_many_tokens(lineno, nt));
     E->src.push_back(in.intern(tok[0]));
     E->dst.push_back(nt == 2 ? in.intern(tok[1]) : -1);
   }
@@ -542,6 +732,8 @@ int write_lines(FILE *f, const prh_edges *e, const double *ranks, Line line) {
 extern "C" {
 
 const char *prh_last_error(void) { return g_err.c_str(); }
+
+void prh_set_read_threads(int32_t n) { g_read_threads = n > 0 ? n : 0; }
 
 int prh_read(const char *path, int32_t format, prh_edges **out) {
   if (!path || !out) return fail("NULL argument");

@@ -49,8 +49,15 @@ def load() -> ctypes.CDLL:
         L.prh_read_ranks.argtypes = [P, ctypes.c_char_p, P]
         L.prh_free.argtypes = [P]
         L.prh_free.restype = None
+        L.prh_set_read_threads.argtypes = [ctypes.c_int32]
+        L.prh_set_read_threads.restype = None
         _hl = L
     return _hl
+
+
+def set_read_threads(n: int) -> None:
+    """Threads of the native edge-list reader (0: automatic); the IDs do not depend on it."""
+    load().prh_set_read_threads(int(n))
 
 
 def _check(rc):

@@ -51,6 +51,57 @@ def test_reader_skips_blank_lines_and_keeps_tokens_verbatim():
     assert src.tolist() == [0, 2] and dst.tolist() == [1, -1]
 
 
+def _read_with_threads(data: bytes, threads: int):
+    from sparky_hip import _host
+
+    _host.set_read_threads(threads)
+    try:
+        e = _host.HostEdges.parse(data)
+        out = (e.names(), e.src.tolist(), e.dst.tolist())
+        e.close()
+        return out
+    finally:
+        _host.set_read_threads(0)
+
+
+@pytest.mark.parametrize("threads", [2, 3, 7, 16])
+def test_chunked_reader_gives_the_sequential_ids(threads):
+    """The multi-threaded edge-list reader (chunks interned locally, merged in chunk order) gives
+    exactly the first-appearance IDs of one thread: blank and CRLF lines, link-less records,
+    names repeated across chunk boundaries, a last line without a newline."""
+    rng = random.Random(threads)
+    lines = []
+    for i in range(3000):
+        r = rng.random()
+        if r < 0.05:
+            lines.append(rng.choice(["", "   ", "\t"]))
+        elif r < 0.15:
+            lines.append(f"u{rng.randrange(400)}")
+        else:
+            a, b = rng.randrange(400), int(rng.paretovariate(1.2)) % 900
+            lines.append(f"u{a}{rng.choice([' ', '  ', chr(9)])}u{b}" + ("\r" if rng.random() < 0.1 else ""))
+    data = "\n".join(lines).encode()  # no trailing newline
+    seq = _read_with_threads(data, 1)
+    assert _read_with_threads(data, threads) == seq
+    names, src, dst = seq
+    ref_names, ref_src, ref_dst = sparky_rdd.intern_first_appearance(
+        sparky_rdd.pairs_from_edge_lines([l.rstrip("\r") for l in lines]))
+    assert names == ref_names and src == ref_src and dst == ref_dst
+
+
+def test_chunked_reader_reports_the_global_line_number():
+    from sparky_hip import _host
+
+    data = ("a b\n" * 500 + "a b c\n" + "c d\n" * 500).encode()
+    for t in (1, 4):
+        _host.set_read_threads(t)
+        try:
+            with pytest.raises(_host.HostError, match="line 501: expected 'src \\[dst\\]', got 3 tokens"):
+                _host.HostEdges.parse(data)
+        finally:
+            _host.set_read_threads(0)
+
+
 def test_part_file_format(tmp_path):
     d = write_part_file(str(tmp_path), 3, ["u1", "u2"], np.array([1.0, 0.7166666666666667]))
     assert os.path.basename(d) == "PageRank3"
