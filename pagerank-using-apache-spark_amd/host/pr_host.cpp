@@ -438,6 +438,7 @@ void gson_to_string(std::string &o, const JVal &v) {
 struct prh_edges {
   std::shared_ptr<void> mapping;     // mmap'd file or copied buffer backing the name views
   std::deque<std::string> arena;     // names created by the JSON front-end
+  std::vector<std::deque<std::string>> chunk_arenas;  // the same, of the parallel reader's chunks
   std::vector<std::string_view> names;
   std::vector<int32_t> src, dst;
 };
@@ -516,10 +517,6 @@ int edge_tokens(const char *data, size_t b, size_t e, std::string_view (&tok)[2]
   return nt;
 }
 
-std::string too_many_tokens(size_t lineno, int nt) {
-  return "line " + std::to_string(lineno) + ": expected 'src [dst]', got " + std::to_string(nt) + " tokens";
-}
-
 int g_read_threads = 0;  // prh_set_read_threads; 0: automatic
 
 // Host threads for the edge-list reader: the affinity mask, capped by the cgroup CPU quota (a GPU
@@ -544,9 +541,11 @@ struct EdgeChunk {
   size_t b = 0, e = 0;
   size_t lines = 0;      // records seen ('\n'-terminated, and a last unterminated one)
   size_t bad_line = 0;   // 1-based line (within the chunk) of the first malformed record, 0: none
-  int bad_tokens = 0;
-  std::vector<int32_t> src, dst;
+  std::string err;       // its message, without the "line N: " prefix
+  std::vector<int32_t> &src, &dst;
+  prh_edges le;          // the chunk's local IDs (src, dst) and JSON-made names (arena)
   std::unique_ptr<Interner> in;
+  EdgeChunk() : src(le.src), dst(le.dst) {}
 };
 
 void parse_edge_chunk(const char *data, EdgeChunk &c) {
@@ -570,9 +569,9 @@ void parse_edge_chunk(const char *data, EdgeChunk &c) {
       if (e > b && data[e - 1] == '\r') --e;
       const int n = edge_tokens(data, b, e, tok[nb]);
       if (n == 0) continue;
-      if (n > 2) {  // the lines before it in this batch are still interned, as sequentially
+        if (n > 2) {  // the lines before it in this batch are still interned, as sequentially
         c.bad_line = c.lines;
-        c.bad_tokens = n;
+        c.err = "expected 'src [dst]', got " + std::to_string(n) + " tokens";
         break;
       }
       nt[nb++] = n;
@@ -589,11 +588,37 @@ void parse_edge_chunk(const char *data, EdgeChunk &c) {
   }
 }
 
+// Common Crawl "url<TAB>json" records of one chunk (Sparky.java:84-118 per record, extract_links)
+void parse_ccjson_chunk(const char *data, EdgeChunk &c) {
+  c.in.reset(new Interner((c.e - c.b) / 256));
+  size_t i = c.b;
+  while (i < c.e) {
+    ++c.lines;
+    const size_t b = i;
+    const char *nl = static_cast<const char *>(std::memchr(data + i, '\n', c.e - i));
+    size_t e = nl ? (size_t)(nl - data) : c.e;
+    i = e + 1;
+    if (e > b && data[e - 1] == '\r') --e;
+    if (e == b) continue;
+    const char *tab = static_cast<const char *>(std::memchr(data + b, '\t', e - b));
+    int rc = 0;
+    if (!tab) rc = fail("line 0: expected 'url<TAB>json'");
+    else rc = extract_links(std::string_view(data + b, (size_t)(tab - (data + b))), tab + 1, data + e, &c.le, *c.in, 0);
+    if (rc != 0) {  // messages are "line <n>: ..."; the chunk's caller puts the file's line number back
+      const std::string &m = g_err;  // this thread's
+      const size_t k = m.find(": ");
+      c.err = (m.rfind("line ", 0) == 0 && k != std::string::npos) ? m.substr(k + 2) : m;
+      c.bad_line = c.lines;
+      return;
+    }
+  }
+}
+
 // Edge list on T threads, IDs exactly those of the sequential reader (first appearance in file
 // order, src before dst): every chunk interns its lines locally in parallel; then the chunks' local
 // name lists are merged in chunk order into the global interner (a name new to chunk c gets its ID
 // in c's local order, which is file order), and the local IDs are translated in parallel.
-int parse_edges_parallel(const char *data, size_t n, int T, prh_edges *E) {
+int parse_parallel(const char *data, size_t n, int32_t format, int T, prh_edges *E) {
   std::vector<size_t> starts{0};
   for (int t = 1; t < T; ++t) {
     const size_t p = n * (size_t)t / (size_t)T;
@@ -610,16 +635,19 @@ int parse_edges_parallel(const char *data, size_t n, int T, prh_edges *E) {
   }
   {
     std::vector<std::thread> th;
-    for (size_t c = 0; c < C; ++c) th.emplace_back(parse_edge_chunk, data, std::ref(ch[c]));
+    for (size_t c = 0; c < C; ++c)
+      th.emplace_back(format == PRH_FORMAT_CCJSON ? parse_ccjson_chunk : parse_edge_chunk, data, std::ref(ch[c]));
     for (auto &t : th) t.join();
   }
   size_t line0 = 0, total = 0, local_names = 0;
   for (size_t c = 0; c < C; ++c) {
-    if (ch[c].bad_line) return fail(too_many_tokens(line0 + ch[c].bad_line, ch[c].bad_tokens));
+    if (ch[c].bad_line) return fail("line " + std::to_string(line0 + ch[c].bad_line) + ": " + ch[c].err);
     line0 += ch[c].lines;
     total += ch[c].src.size();
     local_names += ch[c].in->names().size();
   }
+  for (size_t c = 0; c < C; ++c)  // JSON-made names: moving a deque keeps its elements in place
+    if (!ch[c].le.arena.empty()) E->chunk_arenas.push_back(std::move(ch[c].le.arena));
   if (C == 1) {  // one chunk: its local IDs are the IDs
     E->src.swap(ch[0].src);
     E->dst.swap(ch[0].dst);
@@ -666,39 +694,9 @@ int parse_edges_parallel(const char *data, size_t n, int T, prh_edges *E) {
 }
 
 int parse_into(const char *data, size_t n, int32_t format, prh_edges *E) {
-  if (format == PRH_FORMAT_EDGES) {
-    // large inputs (or an explicit thread count) on several threads; the same IDs either way
-    const int T = g_read_threads > 0 ? g_read_threads : (n >= ((size_t)16 << 20) ? host_threads() : 1);
-    return parse_edges_parallel(data, n, T, E);
-  }
-  Interner in(n / 32);
-  size_t i = 0, lineno = 0;
-  while (i < n) {
-    ++lineno;
-    size_t b = i;
-    while (i < n && data[i] != '\n') ++i;
-    size_t e = i;
-    ++i;
-    if (e > b && data[e - 1] == '\r') --e;
-    if (format == PRH_FORMAT_CCJSON) {
-      if (e == b) continue;
-      const char *tab = static_cast<const char *>(std::memchr(data + b, '\t', e - b));
-      if (!tab) return fail("line " + std::to_string(lineno) + ": expected 'url<TAB>json'");
-      if (extract_links(std::string_view(data + b, (size_t)(tab - (data + b))), tab + 1, data + e, E, in,
-                        lineno) != 0)
-        return -1;
-      continue;
-    }
-    std::string_view tok[2];
-    const int nt = edge_tokens(data, b, e, tok);
-    if (nt == 0) continue;
-    if (nt > 2) return fail(too_many_tokens(lineno, nt));
-    E->src.push_back(in.intern(tok[0]));
-    E->dst.push_back(nt == 2 ? in.intern(tok[1]) : -1);
-  }
-  E->names.swap(in.names());
-  if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
-  return 0;
+  // large inputs (or an explicit thread count) on several threads; the same IDs either way
+  const int T = g_read_threads > 0 ? g_read_threads : (n >= ((size_t)16 << 20) ? host_threads() : 1);
+  return parse_parallel(data, n, format, T, E);
 }
 
 bool mkdirs(const std::string &p) {

@@ -159,3 +159,44 @@ def test_nonexecute_prefix_after_leading_whitespace():
         assert sparky_rdd._parse_json(text) == ("obj", [("a", sparky_rdd._Num("1"))])
     with pytest.raises(ValueError):
         sparky_rdd._parse_json("x )]}'\n{\"a\": 1}")
+
+
+@pytest.mark.parametrize("threads", [2, 5])
+def test_ccjson_chunked_reader_matches_one_thread(threads):
+    """The Common Crawl front-end on several threads (chunks of whole records, merged in chunk
+    order): the same (url, href) pairs, IDs and names as one thread, and errors at the file's line."""
+    from sparky_hip import _host
+
+    rng = random.Random(threads)
+    recs = []
+    for i in range(2000):
+        links = [{"href": f"h{rng.randrange(300)}" + ("\"" if rng.random() < 0.1 else ""),
+                  "type": rng.choice(["a", "a", "img"])} for _ in range(rng.randrange(0, 5))]
+        rec = {"content": {"links": links}} if rng.random() < 0.9 else {}
+        recs.append(f"u{rng.randrange(500)}\t{json.dumps(rec)}")
+        if rng.random() < 0.02:
+            recs.append("")
+    data = "\n".join(recs).encode()
+
+    def read(t, d):
+        _host.set_read_threads(t)
+        try:
+            e = _host.HostEdges.parse(d, "ccjson")
+            out = (e.names(), e.src.tolist(), e.dst.tolist())
+            e.close()
+            return out
+        finally:
+            _host.set_read_threads(0)
+
+    assert read(threads, data) == read(1, data)
+    names, src, dst = read(threads, data)
+    assert [(names[s], None if d < 0 else names[d]) for s, d in zip(src, dst)] == \
+        sparky_rdd.pairs_from_ccjson_lines(recs)
+    bad = data + b"\nu1\t{\"content\": 3}\n"
+    for t in (1, threads):
+        _host.set_read_threads(t)
+        try:
+            with pytest.raises(HostError, match=f"line {len(recs) + 1}: 'content' is not an object"):
+                _host.HostEdges.parse(bad, "ccjson")
+        finally:
+            _host.set_read_threads(0)
