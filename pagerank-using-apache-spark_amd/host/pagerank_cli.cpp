@@ -148,8 +148,10 @@ int run_group(const Options &o, const prh_edges *edges, const double *init, int 
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     double st[PR_STAT_COUNT] = {0};
     if (rc == PR_OK) rc = pr_get_stats(parts[0], st, PR_STAT_COUNT);
-    for (int p = 0; p < P && rc == PR_OK && want; ++p) rc = pr_get_ranks(parts[p], ranks->data());
-    if (rc == PR_OK) on_iter(it, want ? ranks->data() : nullptr, st[PR_STAT_LAST_DC], st[PR_STAT_LAST_L1], ms, job);
+    // ranks to the host only for a part file that is written (every iteration, or the last)
+    const bool fetch = want && (o.save_every || job->start + it == o.iterations - 1);
+    for (int p = 0; p < P && rc == PR_OK && fetch; ++p) rc = pr_get_ranks(parts[p], ranks->data());
+    if (rc == PR_OK) on_iter(it, fetch ? ranks->data() : nullptr, st[PR_STAT_LAST_DC], st[PR_STAT_LAST_L1], ms, job);
   }
   for (int p = 0; p < P && rc == PR_OK; ++p) rc = pr_get_ranks(parts[p], ranks->data());
   const std::string err = rc == PR_OK ? std::string() : std::string(pr_last_error());
@@ -209,8 +211,16 @@ int main(int argc, char **argv) {
     }
     if (n_run > 0) std::printf("Starting iter%d\n", job.start);
     t0 = Clock::now();
-    rc = pr_run(g, n_run, 0.15, 0.85, init_p, ranks.data(), on_iter, o.out.empty() ? 0u : PR_CB_RANKS, &job);
-    ms_run = ms_since(t0);  // iterations, with the per-iteration callback (and its part-file writes)
+    // ranks cross PCIe only for the part files that are written: every iteration's with
+    // --save-every-iter, else only the last one's, which pr_run returns in `ranks` anyway
+    const bool every = !o.out.empty() && o.save_every;
+    rc = pr_run(g, n_run, 0.15, 0.85, init_p, ranks.data(), on_iter, every ? PR_CB_RANKS : 0u, &job);
+    if (rc == PR_OK && !o.out.empty() && !every && n_run > 0 &&
+        prh_write_part(edges, o.out.c_str(), o.iterations - 1, ranks.data()) != 0) {
+      std::fprintf(stderr, "pagerank: %s\n", prh_last_error());
+      job.error = 1;
+    }
+    ms_run = ms_since(t0);  // iterations, with the per-iteration callback and the part-file writes
     pr_graph_destroy(g);
     if (rc != PR_OK) {
       std::fprintf(stderr, "pagerank: run failed (%d): %s\n", rc, pr_last_error());

@@ -89,7 +89,8 @@ def main():
     t0 = time.perf_counter()
     he = HostEdges.read(path)
     t_read = time.perf_counter() - t0
-    threads, desc = bench.host_cores()
+    cands, desc = bench.host_cores()
+    threads = min(cands)  # the granted share (cgroup quota / OMP_NUM_THREADS), not the whole machine
     t0 = time.perf_counter()
     csr = oracle_c.build_csr(he.n_vertices, he.src, he.dst)
     t_build = time.perf_counter() - t0
