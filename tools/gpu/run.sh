@@ -16,6 +16,8 @@
 #   py:<args>         python <args> (a tool script)
 #   pmcpy:<c>:<args>  one rocprofv3 --pmc <c> pass over python <args> (a tool script)
 #   tracepy:<args>    rocprofv3 --kernel-trace --memory-copy-trace --stats -- python3 <args>
+#   dist:<N>:<args>   bench.py --gpus N --share-device <args> under torch.distributed.run (N ranks
+#                     sharing the box's GPU; RCCL over loopback sockets: the N > 1 path for real)
 # Environment variables may prefix a step as KEY=VAL@step (e.g. PR_LIB_PATH=... for an A/B build;
 # the library itself reads no environment: layout choices are bench.py options).
 set -o pipefail
@@ -59,6 +61,10 @@ for step in "$@"; do
       env "${envs[@]}" timeout -k 10 500 python -u $args > $log 2>&1 || exit 1 ;;
     tracepy)
       env "${envs[@]}" timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/trace_$n -o run -- python3 $args > $log 2>&1 || exit 1 ;;
+    dist)
+      N=${arg%%:*}; rest=${arg#*:}; [ "$rest" = "$arg" ] && rest=""
+      env "${envs[@]}" timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N \
+        --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $N --share-device ${rest//,/ } > $log 2>&1 || exit 1 ;;
     *)
       echo "unknown step $name" >&2; exit 2 ;;
   esac
