@@ -655,21 +655,75 @@ int parse_parallel(const char *data, size_t n, int32_t format, int T, prh_edges 
     if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
     return 0;
   }
-  Interner g(std::max(local_names / 2, (size_t)1024));
+  // Merge, sharded by hash over C threads.  Shard s walks every chunk's local names in chunk order
+  // and keeps those whose hash it owns: the first time it sees a name, (c, k) is that name's first
+  // appearance in the file (chunk order, then local order); otherwise it records where the name
+  // first appeared.  A name new at (c, k) then gets ID base[c] + (the names new in c before k),
+  // base[c] = the names new in chunks < c: exactly the sequential first-appearance numbering.
+  const size_t S = C;
+  std::vector<std::vector<uint8_t>> isnew(C);
+  std::vector<std::vector<uint64_t>> first(C);  // (c0 << 32) | k0 of the name's first appearance
+  for (size_t c = 0; c < C; ++c) {
+    isnew[c].assign(ch[c].in->names().size(), 0);
+    first[c].resize(ch[c].in->names().size());
+  }
+  {
+    std::vector<std::thread> th;
+    for (size_t sh = 0; sh < S; ++sh)
+      th.emplace_back([&, sh]() {
+        Interner g(std::max(local_names / (2 * S), (size_t)1024));
+        std::vector<uint64_t> where;  // per shard-local ID: its first (c, k)
+        for (size_t c = 0; c < C; ++c) {
+          const auto &nm = ch[c].in->names();
+          const auto &hs = ch[c].in->hashes();
+          for (size_t k = 0; k < nm.size(); ++k) {
+            if ((hs[k] >> 40) % S != sh) continue;
+            const size_t before = g.names().size();
+            const int32_t id = g.intern_hashed(nm[k], hs[k]);
+            if ((size_t)id == before) {  // new: its first appearance
+              where.push_back((uint64_t)c << 32 | k);
+              isnew[c][k] = 1;
+            }
+            first[c][k] = where[(size_t)id];
+          }
+        }
+      });
+    for (auto &t : th) t.join();
+  }
+  std::vector<size_t> base(C + 1, 0);
   std::vector<std::vector<int32_t>> to_global(C);
   for (size_t c = 0; c < C; ++c) {
-    const auto &nm = ch[c].in->names();
-    const auto &hs = ch[c].in->hashes();
-    to_global[c].resize(nm.size());
-    constexpr size_t kB = 32;  // batches with prefetched slots and names, as in parse_edge_chunk
-    for (size_t k0 = 0; k0 < nm.size(); k0 += kB) {
-      const size_t k1 = std::min(nm.size(), k0 + kB);
-      for (size_t k = k0; k < k1; ++k) g.prefetch_slot(hs[k]);
-      for (size_t k = k0; k < k1; ++k) g.prefetch_name(hs[k]);
-      for (size_t k = k0; k < k1; ++k) to_global[c][k] = g.intern_hashed(nm[k], hs[k]);
-    }
-    ch[c].in.reset();  // the views stay valid: they point into the input
+    size_t cnt = 0;
+    for (uint8_t f : isnew[c]) cnt += f;
+    base[c + 1] = base[c] + cnt;
   }
+  if (base[C] > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
+  E->names.resize(base[C]);
+  {
+    std::vector<std::thread> th;  // IDs of the names new in each chunk
+    for (size_t c = 0; c < C; ++c)
+      th.emplace_back([&, c]() {
+        const auto &nm = ch[c].in->names();
+        to_global[c].assign(nm.size(), -1);
+        int32_t id = (int32_t)base[c];
+        for (size_t k = 0; k < nm.size(); ++k)
+          if (isnew[c][k]) {
+            E->names[(size_t)id] = nm[k];
+            to_global[c][k] = id++;
+          }
+      });
+    for (auto &t : th) t.join();
+  }
+  {
+    std::vector<std::thread> th;  // the others: the ID of their first appearance
+    for (size_t c = 0; c < C; ++c)
+      th.emplace_back([&, c]() {
+        for (size_t k = 0; k < to_global[c].size(); ++k)
+          if (!isnew[c][k]) to_global[c][k] = to_global[first[c][k] >> 32][first[c][k] & 0xFFFFFFFFull];
+      });
+    for (auto &t : th) t.join();
+  }
+  for (size_t c = 0; c < C; ++c) ch[c].in.reset();  // the views stay valid: they point into the input
   E->src.resize(total);
   E->dst.resize(total);
   {
@@ -688,8 +742,6 @@ int parse_parallel(const char *data, size_t n, int32_t format, int T, prh_edges 
     }
     for (auto &t : th) t.join();
   }
-  E->names.swap(g.names());
-  if (E->names.size() > (size_t)INT32_MAX) return fail("more than 2^31-1 distinct URLs");
   return 0;
 }
 
