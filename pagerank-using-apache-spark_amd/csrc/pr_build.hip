@@ -362,17 +362,19 @@ __global__ __launch_bounds__(256) void k_fill_hot(int64_t n_units, const Unit *_
   atomicAdd(n_hot, nh);
 }
 
-// Compact entry codes (pr_internal.h kCodeC20, P = 1): one thread per 8-entry lane group of a wave
-// unit writes the group's 8 u16 low index halves and its side word (end marks, high bits).  A
-// source at region offset o of class x (gather position x*Q_pad + o) has index o + 1; padding 0.
-// *n_hot counts the entries that read the LDS hot set; *bad the sources outside the unit's region
-// band (none by construction: the codes would then read another class's values).
-__global__ __launch_bounds__(64) void k_fill_c20(int64_t n_units, const Unit *__restrict__ units,
-                                                 const int64_t *__restrict__ src_off,
-                                                 const int32_t *__restrict__ n_real, const int32_t *__restrict__ col,
-                                                 int64_t Q_pad, int q_load, uint16_t *__restrict__ code16,
-                                                 uint32_t *__restrict__ cside, unsigned long long *n_hot,
-                                                 unsigned long long *bad) {
+// Compact entry codes (pr_internal.h kCodeC20 / kCodeC24, P = 1): one thread per 8-entry lane
+// group of a wave unit writes the group's 8 u16 low index halves and its side word (end marks,
+// HB high bits per entry: u32 for 3, u64 for 4).  A source at region offset o of class x (gather
+// position x*Q_pad + o) has index o + 1; padding 0.  *n_hot counts the entries that read the LDS
+// hot set; *bad the sources outside the unit's region band (none by construction: the codes would
+// then read another class's values).
+template <int HB, class SideT>
+__global__ __launch_bounds__(64) void k_fill_compact(int64_t n_units, const Unit *__restrict__ units,
+                                                     const int64_t *__restrict__ src_off,
+                                                     const int32_t *__restrict__ n_real,
+                                                     const int32_t *__restrict__ col, int64_t Q_pad, int q_load,
+                                                     uint16_t *__restrict__ code16, SideT *__restrict__ cside,
+                                                     unsigned long long *n_hot, unsigned long long *bad) {
   unsigned long long nh = 0, nb = 0;
   for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
     const Unit u = units[b];
@@ -381,7 +383,8 @@ __global__ __launch_bounds__(64) void k_fill_c20(int64_t n_units, const Unit *__
     int64_t x0 = -1;  // the unit's class: the region of its first source
     if (n > 0) x0 = (int64_t)(col[s0] & 0x7FFFFFFF) / Q_pad;
     for (int grp = threadIdx.x; grp < u.n / 8; grp += 64) {
-      uint32_t side = 0, lo[8];
+      SideT side = 0;
+      uint32_t lo[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int i = 8 * grp + j;
@@ -393,10 +396,10 @@ __global__ __launch_bounds__(64) void k_fill_c20(int64_t n_units, const Unit *__
           nb += x != x0 ? 1 : 0;
           idx = (uint32_t)(pos - x * Q_pad + 1);
           nh += idx <= (uint32_t)q_load ? 1 : 0;
-          if (u.meta >= 0 && v < 0) side |= 1u << j;  // segment end (STREAM units)
+          if (u.meta >= 0 && v < 0) side |= (SideT)1 << j;  // segment end (STREAM units)
         }
         lo[j] = idx & 0xFFFFu;
-        side |= ((idx >> 16) & 7u) << (8 + 3 * j);
+        side |= (SideT)((idx >> 16) & ((1u << HB) - 1u)) << (8 + HB * j);
       }
       uint4 q;
       q.x = lo[0] | lo[1] << 16;
@@ -709,12 +712,16 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     // compact codes when every region index fits (P = 1: a class's sources are its region of the
-    // one slice; a part of a row partition also reads received runs, so it keeps 32-bit codes)
-    const bool c20 = g->opts.codes != 0 && P == 1 && g->gsize == g->S_pad && g->Q_pad < (int64_t(1) << kC20IdxBits);
-    g->code = c20 ? kCodeC20 : kCodeU32;
-    if (c20) {
+    // one slice; a part of a row partition also reads received runs, so it keeps 32-bit codes):
+    // 2.5 bytes per entry below 2^19 region rows, 3 below 2^20
+    const bool compact = g->opts.codes != 0 && P == 1 && g->gsize == g->S_pad;
+    g->code = compact && g->Q_pad < (int64_t(1) << kC20IdxBits)   ? kCodeC20
+              : compact && g->Q_pad < (int64_t(1) << kC24IdxBits) ? kCodeC24
+                                                                   : kCodeU32;
+    const bool c20 = g->code == kCodeC20, c24 = g->code == kCodeC24;
+    if (c20 || c24) {
       PR_TRY(g->colh.alloc(sizeof(uint16_t) * (sp.entries > 0 ? sp.entries : 8)));
-      PR_TRY(g->cside.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries / 8 : 1)));
+      PR_TRY(g->cside.alloc((c24 ? sizeof(uint64_t) : sizeof(uint32_t)) * (sp.entries > 0 ? sp.entries / 8 : 1)));
     } else {
       PR_TRY(g->colh.alloc(sizeof(uint32_t) * (sp.entries > 0 ? sp.entries : 8)));
       PR_TRY(g->cside.alloc(sizeof(uint32_t)));
@@ -727,10 +734,15 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     if (nu > 0) {
       PR_HIP(hipMemsetAsync(cnt.p, 0, 2 * sizeof(unsigned long long), s));
       if (c20)
-        hipLaunchKernelGGL(k_fill_c20, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(64), 0, s, nu,
-                           g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
+        hipLaunchKernelGGL((k_fill_compact<3, uint32_t>), dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(64), 0, s,
+                           nu, g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
                            g->col.as<int32_t>(), g->Q_pad, hg.q_load, g->colh.as<uint16_t>(),
                            g->cside.as<uint32_t>(), cnt.as<unsigned long long>(), cnt.as<unsigned long long>() + 1);
+      else if (c24)
+        hipLaunchKernelGGL((k_fill_compact<4, uint64_t>), dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(64), 0, s,
+                           nu, g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
+                           g->col.as<int32_t>(), g->Q_pad, hg.q_load, g->colh.as<uint16_t>(),
+                           g->cside.as<uint64_t>(), cnt.as<unsigned long long>(), cnt.as<unsigned long long>() + 1);
       else
         hipLaunchKernelGGL(k_fill_hot, dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(256), 0, s, nu,
                            g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),

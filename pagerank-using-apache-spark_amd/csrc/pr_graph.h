@@ -78,7 +78,8 @@ struct pr_graph {
   // segment of every 64-row block (cbase[blk][x]); long segments: pieces reduced in order into
   // partial[seg_slot[q]]; hpos[x * P*Kp + i]: gather position of LDS hot slot 1 + i of class x
   pr::DevBuf colh, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
-  // entry code format (pr_internal.h): kCodeU32 (colh = u32 codes) or kCodeC20 (colh = u16 low
+  // entry code format (pr_internal.h): kCodeU32 (colh = u32 codes), kCodeC24 (as C20 with a u64
+  // side word and 4 high bits per entry) or kCodeC20 (colh = u16 low
   // index bits, cside = one u32 of end marks and high bits per 8 entries)
   int code = pr::kCodeU32;
   pr::DevBuf cside;

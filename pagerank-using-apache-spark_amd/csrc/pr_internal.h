@@ -145,11 +145,16 @@ constexpr uint32_t kEntZero = 0u;  // LDS slot 0
 //   code16[8]  u16: the low 16 bits of idx (one 16-byte load per lane)
 //   side       u32: bits 0-7 the segment-end marks of the 8 entries, bits 8 + 3j .. 10 + 3j the
 //              high 3 bits of entry j's idx (one 4-byte load per lane)
-// -> 2.5 B per in-link, idx < 2^19 (R-MAT s26: Q_pad = 512640).  Larger class regions, and parts
-// of a row partition (whose class sources span several received runs), keep the 32-bit codes.
+// -> 2.5 B per in-link, idx < 2^19 (R-MAT s26: Q_pad = 512640).  Class regions up to 2^20 rows
+// (the Twitter shape: Q_pad = 650816) take the 3-byte variant kCodeC24: a u64 side word per lane,
+// bits 0-7 the end marks, bits 8 + 4j .. 11 + 4j the high 4 bits of idx (one 8-byte load).  Larger
+// class regions, and parts of a row partition (whose class sources span several received runs),
+// keep the 32-bit codes.
 constexpr int kCodeU32 = 0;
 constexpr int kCodeC20 = 1;
+constexpr int kCodeC24 = 2;
 constexpr int kC20IdxBits = 19;
+constexpr int kC24IdxBits = 20;
 // LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part), one
 // more 0.0 slot (where compact cold entries point their LDS read), the workgroup's unit counter,
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by

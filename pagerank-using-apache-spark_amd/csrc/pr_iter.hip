@@ -160,7 +160,8 @@ int prepare_hot_kernel() {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
   for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>)})
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>)})
     PR_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   return PR_OK;
 }
@@ -226,7 +227,9 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   if (ph1 < 0) ph1 = n_hot_phases(g);
   const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
-  auto kern = g->code == kCodeC20 ? k_spmv_hot<kCodeC20> : k_spmv_hot<kCodeU32>;
+  auto kern = g->code == kCodeC20   ? k_spmv_hot<kCodeC20>
+              : g->code == kCodeC24 ? k_spmv_hot<kCodeC24>
+                                    : k_spmv_hot<kCodeU32>;
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),

@@ -336,6 +336,26 @@ __device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint16_t *_
   w.s = __builtin_amdgcn_raw_buffer_load_b32(rsd, lane_id() * 4, 0, 2);
 }
 
+// 3-byte codes (kCodeC24, class regions up to 2^20 rows): the same low halves and a u64 side word
+// (8 end marks, 4 high bits per entry; one 8-byte load).
+struct WaveCodesC24 {
+  uint32_t w[kWavePT / 2];
+  uint64_t s;
+};
+__device__ __forceinline__ void wave_unit_codes(const Unit &u, const uint16_t *__restrict__ code16,
+                                                const uint64_t *__restrict__ cside, WaveCodesC24 &w) {
+  const __amdgpu_buffer_rsrc_t rm =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(code16 + (int64_t)u.p8 * 8), 0, u.n * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsd =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(cside + (int64_t)u.p8), 0, u.n, 0x00020000);
+  const pr_v4i x = __builtin_bit_cast(pr_v4i, __builtin_amdgcn_raw_buffer_load_b128(rm, lane_id() * 16, 0, 2));
+  w.w[0] = (uint32_t)x.x;
+  w.w[1] = (uint32_t)x.y;
+  w.w[2] = (uint32_t)x.z;
+  w.w[3] = (uint32_t)x.w;
+  w.s = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rsd, lane_id() * 8, 0, 2));
+}
+
 // Which of the lane's entries end a segment (bit j: entry j).
 __device__ __forceinline__ uint32_t end_marks(const WaveCodes &w) {
   uint32_t endm = 0;
@@ -344,6 +364,7 @@ __device__ __forceinline__ uint32_t end_marks(const WaveCodes &w) {
   return endm;
 }
 __device__ __forceinline__ uint32_t end_marks(const WaveCodesC20 &w) { return w.s & 0xFFu; }
+__device__ __forceinline__ uint32_t end_marks(const WaveCodesC24 &w) { return (uint32_t)w.s & 0xFFu; }
 
 // The lane metadata of a STREAM unit from the end marks of its entries: which of the lane's
 // entries end a segment, the index (within the unit) of the lane's first segment end (an
@@ -403,6 +424,20 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
   for (int j = 0; j < kWavePT; ++j) {
     const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
     const uint32_t idx = lo | (((w.s >> (8 + 3 * j)) & 7u) << 16);
+    const uint32_t b8 = idx << 3;
+    const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
+    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, b8 - cs.hb, 0, 0));
+    v[j] = __dadd_rn(a, b);
+  }
+}
+
+__device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const double *hot, const ClassSrc &cs,
+                                                 double (&v)[kWavePT]) {
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) {
+    const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
+    const uint32_t idx = lo | ((uint32_t)(w.s >> (8 + 4 * j)) & 15u) << 16;
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
@@ -492,7 +527,8 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, con
   }
 }
 
-// The code streams of a part (pr_internal.h): 32-bit codes, or compact low halves + side words.
+// The code streams of a part (pr_internal.h): 32-bit codes, or compact low halves + side words
+// (u32 per 8 entries for kCodeC20, u64 for kCodeC24).
 struct CodeSrc {
   const void *codes;
   const uint32_t *side;
@@ -505,9 +541,15 @@ template <>
 struct CodeOf<kCodeC20> {
   using T = WaveCodesC20;
 };
+template <>
+struct CodeOf<kCodeC24> {
+  using T = WaveCodesC24;
+};
 template <int CODE>
 __device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typename CodeOf<CODE>::T &w) {
   if constexpr (CODE == kCodeC20) wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), cd.side, w);
+  else if constexpr (CODE == kCodeC24)
+    wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), reinterpret_cast<const uint64_t *>(cd.side), w);
   else wave_unit_codes(u, static_cast<const uint32_t *>(cd.codes), w);
 }
 
@@ -594,13 +636,13 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
   ClassSrc cs;
   cs.zb = (uint32_t)hg.slots() * 8u;
   cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
-  if constexpr (CODE != kCodeC20) cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+  if constexpr (CODE == kCodeU32) cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int team = (int)(blockIdx.x / kXcds), nteams = (int)(gridDim.x / kXcds);
   for (int ph = ph0; ph < ph1; ++ph) {
     const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
-    if constexpr (CODE == kCodeC20) {  // region index q_load + 1 + k -> position x*Q_pad + q_load + k
+    if constexpr (CODE != kCodeU32) {  // region index q_load + 1 + k -> position x*Q_pad + q_load + k
       const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;
       cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0,
                                                  (uint32_t)((hg.Q_pad - hg.q_load) * 8), 0x00020000);

@@ -588,14 +588,21 @@ def test_compact_codes_bitwise(hip, oracle_c, classes, slots):
         assert g.info()["code_bits"] == 32
 
 
-def test_compact_codes_fall_back_for_large_regions(hip, oracle_c):
-    """A class region of 2^19 rows or more does not fit the compact index: 32-bit codes, same
-    ranks as the oracle."""
+@pytest.mark.parametrize("V,bits", [(4400000, 24), (8800000, 32)])
+def test_compact_codes_widen_then_fall_back(hip, oracle_c, V, bits):
+    """Class regions of 2^19..2^20 rows (8 classes over 4.4 M vertices: Q_pad > 2^19) take the
+    3-byte codes (kCodeC24: u64 side word, 4 high bits per entry), bitwise the ranks of the 32-bit
+    codes; regions of 2^20 rows or more keep the 32-bit codes.  Both match the oracle."""
     rng = np.random.default_rng(77)
-    V = 4400000  # 8 classes -> Q_pad > 2^19
-    src, dst = random_edges(rng, V, 4000000)
+    src, dst = random_edges(rng, V, 4000000, hub_frac=0.01)
     csr, ref, ranks, stats, hist, info = run_both(hip, oracle_c, V, src, dst, 4, layout="split",
                                                   options={"classes": 8})
-    assert info["code_bits"] == 32
+    assert info["code_bits"] == bits
     for it in range(4):
         assert max_rel(hist[it], ref["history"][it]) <= RANK_TOL, it
+    if bits == 24:
+        with hip.PageRankGraph(V, src, dst, layout="split", keep_canonical=False,
+                               options={"classes": 8, "codes": 0}) as g:
+            assert g.info()["code_bits"] == 32
+            r32, _ = g.run(4)
+        assert np.array_equal(r32, ranks)
