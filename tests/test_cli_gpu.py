@@ -66,6 +66,28 @@ def test_cli_edge_list(tmp_path, runner):
             assert abs(part[u] - v) <= 1e-9 * v
 
 
+def test_cli_writes_only_the_last_part_and_reports_the_job(tmp_path):
+    """Without --save-every-iter only PageRank<N-1> is written (Sparky.java:237 for the last
+    iteration; its ranks are the ones pr_run returns, no per-iteration copy), and --stats reports
+    the job's phases as one JSON object on stderr."""
+    inp = tmp_path / "edges.txt"
+    inp.write_text("\n".join(KAT) + "\n")
+    out_dir = tmp_path / "out"
+    res = subprocess.run([CLI, str(inp), "4", "--out", str(out_dir), "--stats"], capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert sorted(os.listdir(out_dir)) == ["PageRank3"]
+    hist = oracle(sparky_rdd.pairs_from_edge_lines(KAT), 4)
+    part = parse_part(out_dir / "PageRank3" / "part-00000")
+    assert part.keys() == hist[-1].keys()
+    for u, v in hist[-1].items():
+        assert abs(part[u] - v) <= 1e-9 * v
+    assert parse_has_rank(res.stdout) == part
+    job = json.loads([l for l in res.stderr.splitlines() if l.startswith('{"job"')][-1])["job"]
+    assert job["urls"] == len(hist[-1]) and job["edge_records"] == len(KAT) and job["iterations"] == 4
+    assert all(job[k] >= 0 for k in ("read_intern_ms", "build_ms", "run_ms", "has_rank_out_ms", "total_ms"))
+
+
 def test_cli_ccjson(tmp_path):
     rng = np.random.default_rng(2)
     recs = []
