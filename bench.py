@@ -28,6 +28,10 @@ Rank 0 prints ONE JSON line (the driver's contract), including
                   next iteration's SpMV phases (pr_set_option) with 0/1/2 CUs per XCD kept free for
                   the transfer kernels; the fastest mode is the one timed (config.exchange_mode);
                   the parity leg checks both exchange modes.
+  --share-device: a rehearsal of the N > 1 path on a box with fewer GPUs than ranks (every rank
+                  on device rank % count, RCCL over loopback sockets via a per-rank NCCL_HOSTID);
+                  config.shared_device_rehearsal marks such a line: its parity is real, its speed
+                  is the sockets'.
 """
 from __future__ import annotations
 
