@@ -201,6 +201,9 @@ def main() -> int:
                          "device r %% count and poses to RCCL as a host of its own (NCCL_HOSTID), so RCCL's "
                          "duplicate-GPU check passes and the ranks talk over its socket transport on "
                          "loopback -- the library's RCCL exchange executes for real; its speed means nothing")
+    ap.add_argument("--serial-build", action="store_true",
+                    help="N > 1: ranks generate and build their parts one after another (with --share-device: "
+                         "one edge list on the device at a time)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -238,20 +241,33 @@ def main() -> int:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", dev))
 
-    wd.enter("generate", limits["generate"])
-    t0 = time.perf_counter()
-    wl = generate(a.graph, scale=a.scale, edge_factor=a.edge_factor, seed=a.seed, device=dev)
-    V, E, workload = wl.n_vertices, wl.n_edges, wl.description
-    t_gen = time.perf_counter() - t0
-    log(f"rank {rank}: generated + interned {E} edges, V={V} in {t_gen:.2f}s")
     validate = not a.no_cpu_baseline
-    wd.enter("build", limits["build"])
     bopts = {k: int(v) for k, v in (o.split("=", 1) for o in a.build_option)}
-    g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
-                                 n_edges=E, part=rank, n_parts=world, keep_canonical=(validate and rank == 0),
-                                 layout=a.layout, options=bopts)
-    del wl
-    torch.cuda.empty_cache()
+
+    def generate_and_build():
+        wd.enter("generate", limits["generate"])
+        t0 = time.perf_counter()
+        wl = generate(a.graph, scale=a.scale, edge_factor=a.edge_factor, seed=a.seed, device=dev)
+        V, E, workload = wl.n_vertices, wl.n_edges, wl.description
+        log(f"rank {rank}: generated + interned {E} edges, V={V} in {time.perf_counter() - t0:.2f}s")
+        wd.enter("build", limits["build"])
+        g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
+                                     n_edges=E, part=rank, n_parts=world, keep_canonical=(validate and rank == 0),
+                                     layout=a.layout, options=bopts)
+        del wl
+        torch.cuda.empty_cache()
+        return g, V, E, workload
+
+    if a.serial_build and dist is not None:
+        # ranks sharing one GPU (--share-device) generate and build one after another, so only one
+        # whole edge list and one build's temporaries are on the device at a time
+        for r in range(world):
+            if r == rank:
+                g, V, E, workload = generate_and_build()
+            wd.enter("build", limits["build"])
+            dist.barrier()
+    else:
+        g, V, E, workload = generate_and_build()
     info = g.info()
     log(f"rank {rank}: build {g.stats()['build_ms']:.0f} ms; info {info}")
     if world > 1:
