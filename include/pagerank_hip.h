@@ -129,8 +129,9 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_HOT_RESERVE 5 /* CUs per XCD the heavy SpMV kernel leaves free, 0..3 (PR_OPT_HOT_RESERVE) */
 #define PR_BOPT_EPI_WALK 6    /* split layout: 1 (default) per-row walk of sparse epilogue groups, 0 never */
 #define PR_BOPT_EPI_NARROW 7  /* split layout: -1 auto (default), 0 four-wave, 1 one-wave epilogue workgroups */
-#define PR_BOPT_CODES 8       /* split layout: -1 (default) 2.5-byte entry codes where they fit (P = 1, class
-                                 regions < 2^19 positions), 0 always 4-byte codes; same sums either way */
+#define PR_BOPT_CODES 8       /* split layout: -1 (default) compact entry codes where they fit (P = 1: 2.5 bytes
+                                 for class regions < 2^19 positions, 3 bytes < 2^20), 0 always 4-byte codes;
+                                 same sums either way (PR_INFO code_bits: 20 / 24 / 32) */
 int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
                        const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
                        int32_t n_options, pr_graph **out);
