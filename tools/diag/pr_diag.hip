@@ -91,6 +91,28 @@ __global__ __launch_bounds__(256) void k_stream_probe(char *__restrict__ table, 
   }
   if (acc == 12345u) out[t] = acc;
 }
+// Scalar-path probe: every wave issues `per_wave` random 8-byte loads from uniform (wave-wide)
+// addresses, which the compiler turns into s_load_dwordx2 through the scalar data cache (not the
+// vector memory path the gathers of k_spmv_hot saturate).  Loads per second say whether the
+// scalar path could carry a share of the cold gathers.
+template <int UNROLL>
+__global__ __launch_bounds__(256) void k_scalar_probe(const double *__restrict__ table, uint32_t n_words,
+                                                      int64_t n_waves, int per_wave, uint32_t seed,
+                                                      double *__restrict__ out) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_waves) return;
+  const __attribute__((address_space(4))) double *ct = (const __attribute__((address_space(4))) double *)table;
+  const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane((int)w);
+  double acc = 0.0;
+  for (int j0 = 0; j0 < per_wave; j0 += UNROLL) {
+    double v[UNROLL];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) v[k] = ct[mix32(wu * 4099u + (uint32_t)(j0 + k) + seed) % n_words];
+#pragma unroll
+    for (int k = 0; k < UNROLL; ++k) acc += v[k];
+  }
+  if (acc == 12345.0 && (threadIdx.x & 63) == 0) out[w] = acc;
+}
 // CU-mask probe: every workgroup (one wave) records its XCC id and raw HW_ID register (CU, SH, SE
 // fields), so a stream's CU-mask bits can be mapped to physical CUs and XCDs.
 __global__ void k_cu_probe(uint32_t *__restrict__ out) {
@@ -228,6 +250,38 @@ int prd_stream_probe(int device, int64_t table_bytes, int64_t n_loads, int width
         else hipLaunchKernelGGL((k_stream_probe<16, false>), grid, dim3(256), 0, 0, T, tb, nt, active, O);
       }
     }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
+  return 0;
+}
+
+// Scalar-path probe (see k_scalar_probe): n_loads uniform random loads in total; returns ms.
+int prd_scalar_probe(int device, int64_t table_bytes, int64_t n_loads, int per_wave, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  void *tab = nullptr, *out = nullptr;
+  PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8 * 1024 * 1024));
+  const int64_t nw = n_loads / per_wave;
+  const uint32_t nwords = (uint32_t)(table_bytes / 8);
+  const dim3 grid((unsigned)((nw + 3) / 4));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i)
+      hipLaunchKernelGGL(k_scalar_probe<8>, grid, dim3(256), 0, 0, (const double *)tab, nwords, nw, per_wave,
+                         977u * (uint32_t)i, (double *)out);
     PR_HIP(hipGetLastError());
     PR_HIP(hipEventRecord(b, 0));
     PR_HIP(hipEventSynchronize(b));
