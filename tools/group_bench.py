@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--parts", default="2,4,8")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--allgather", action="store_true")
+    ap.add_argument("--build-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="pr_graph_create_ex option of every part (P > 1), e.g. hot_slots=9000; repeatable")
     a = ap.parse_args()
     E = a.edge_factor << a.scale
     s = torch.empty(E, dtype=torch.int32, device="cuda")
@@ -40,7 +42,9 @@ def main():
     def run(P):
         parts = [sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, part=p,
                                           n_parts=P, keep_canonical=False,
-                                          options={"exchange_allgather": int(a.allgather)}) for p in range(P)]
+                                          options=dict({"exchange_allgather": int(a.allgather)},
+                                                       **({k: int(v) for k, v in (o.split("=", 1) for o in a.build_option)}
+                                                          if P > 1 else {}))) for p in range(P)]
         try:
             infos = [p.info() for p in parts]
             if P == 1:
