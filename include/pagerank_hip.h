@@ -132,6 +132,9 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_CODES 8       /* split layout: -1 (default) compact entry codes where they fit (P = 1: 2.5 bytes
                                  for class regions < 2^19 positions, 3 bytes < 2^20), 0 always 4-byte codes;
                                  same sums either way (PR_INFO code_bits: 20 / 24 / 32) */
+#define PR_BOPT_PACK_FUSED 9  /* P > 1 (per-peer runs, split layout): 1 (default) the epilogue writes the
+                                 contributions every peer reads straight into the send runs, 0 a separate
+                                 pack kernel gathers them after the pass; same values either way */
 int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
                        const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
                        int32_t n_options, pr_graph **out);

@@ -112,6 +112,35 @@ __global__ __launch_bounds__(256) void k_pack(int64_t n, const uint32_t *__restr
   }
 }
 
+// Fused pack (pr_graph.h x_fused): pmask[row] bit q = peer q reads the row (its send run lists
+// it); sbase[blk * P + q] = entries of peer q's run (slots excluded) at rows < 64 blk, so the
+// epilogue stores lane L's c' at run q + sbase + (lanes below L with bit q).  One launch per peer:
+// a peer's positions are unique, so the byte updates of one launch never collide.
+__global__ void k_pmask(int64_t n, const uint32_t *__restrict__ pos, uint8_t bit, uint8_t *__restrict__ pmask) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    pmask[pos[i]] |= bit;
+}
+__global__ void k_sbase(int64_t nblk, int P, int self, const uint32_t *__restrict__ send,
+                        const int64_t *__restrict__ soff, int32_t *__restrict__ sbase) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nblk * P; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t blk = t / P;
+    const int q = (int)(t - blk * P);
+    int64_t r = 0;
+    if (q != self) {
+      const int64_t b = soff[q], e = soff[q + 1] - 2;  // the run without its two slots
+      const uint32_t target = (uint32_t)(blk * kWave);
+      int64_t lo = b, hi = e;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (send[mid] < target) lo = mid + 1;
+        else hi = mid;
+      }
+      r = lo - b;
+    }
+    sbase[t] = (int32_t)r;
+  }
+}
+
 // Compacted gather space: global position -> this part's position (-1: never read here).
 __global__ void k_cmap_own(int64_t S_pad, int part, int32_t *__restrict__ cmap) {
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < S_pad; j += (int64_t)gridDim.x * blockDim.x)
@@ -200,6 +229,31 @@ int build_list(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t ma
   return PR_OK;
 }
 
+int build_fused_pack(pr_graph *g) {
+  const int P = g->nparts;
+  hipStream_t s = g->stream;
+  const int64_t nblk = (g->n_rows + kWave - 1) / kWave;  // the epilogue's 64-row blocks (g->nblk)
+  const int64_t rows = nblk * kWave;
+  DevBuf doff;
+  PR_TRY(doff.alloc(sizeof(int64_t) * (P + 1)));
+  PR_TRY(g->x_pmask.alloc((size_t)rows));
+  PR_TRY(g->x_sbase.alloc(sizeof(int32_t) * (size_t)(nblk * P)));
+  PR_HIP(hipMemcpyAsync(doff.p, g->x_soff.data(), sizeof(int64_t) * (P + 1), hipMemcpyHostToDevice, s));
+  PR_HIP(hipMemsetAsync(g->x_pmask.p, 0, (size_t)rows, s));
+  for (int q = 0; q < P; ++q) {
+    const int64_t n = g->x_soff[q + 1] - 2 - g->x_soff[q];
+    if (q == g->part || n <= 0) continue;
+    hipLaunchKernelGGL(k_pmask, dim3(grid_for(n, 256, 65536)), dim3(256), 0, s, n,
+                       g->x_send.as<uint32_t>() + g->x_soff[q], (uint8_t)(1u << q), g->x_pmask.as<uint8_t>());
+  }
+  hipLaunchKernelGGL(k_sbase, dim3(grid_for(nblk * P, 256, 65536)), dim3(256), 0, s, nblk, P, g->part,
+                     g->x_send.as<uint32_t>(), doff.as<int64_t>(), g->x_sbase.as<int32_t>());
+  PR_HIP(hipGetLastError());
+  PR_HIP(hipStreamSynchronize(s));
+  g->x_fused = true;
+  return PR_OK;
+}
+
 }  // namespace
 
 // doubles per send buffer, even so that the second buffer stays 16-byte aligned (k_pack)
@@ -255,6 +309,9 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   g->x_ev.assign(g->n_xc, nullptr);
   for (auto &e : g->x_ev) PR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   PR_HIP(hipEventCreateWithFlags(&g->x_pack_ev, hipEventDisableTiming));
+  // fused pack: the split epilogue writes the runs itself (P <= 8: the row mask is one byte)
+  g->x_fused = false;
+  if (g->opts.pack_fused && g->C > 1 && P <= kMaxPackParts && g->x_soff[P] > 0) PR_TRY(build_fused_pack(g));
   return PR_OK;
 }
 
@@ -305,7 +362,8 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
     if (ev_b) PR_HIP(hipEventRecord(ev_b, g->stream));
     return PR_OK;
   }
-  PR_TRY(exchange_pack(g, buf));
+  if (g->x_packed != buf) PR_TRY(exchange_pack(g, buf));  // else the epilogue wrote the runs
+  g->x_packed = -1;
   PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
   PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
   if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
@@ -343,7 +401,8 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
   const bool whole = parts[0]->x_allgather;
   for (int p = 0; p < n; ++p) {
     PR_HIP(hipSetDevice(parts[p]->device));
-    if (!whole) PR_TRY(exchange_pack(parts[p], buf));
+    if (!whole && parts[p]->x_packed != buf) PR_TRY(exchange_pack(parts[p], buf));
+    parts[p]->x_packed = -1;
     PR_HIP(hipEventRecord(whole ? parts[p]->xev : parts[p]->x_pack_ev, parts[p]->stream));
   }
   for (int q = 0; q < n; ++q) {

@@ -41,6 +41,7 @@ struct pr_build_opts {
   bool epi_walk = true;
   int epi_narrow = -1;   // -1: by the share of walking groups
   int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
+  bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
 };
 
 struct pr_graph {
@@ -144,6 +145,14 @@ struct pr_graph {
   std::vector<hipEvent_t> x_ev;
   hipEvent_t x_pack_ev = nullptr;
   bool x_pending = false;
+  // Fused pack (PR_BOPT_PACK_FUSED, split layout, per-peer runs, P <= 8): per local row the peers
+  // that read it (x_pmask, bit q), per 64-row block and peer the index of the block's first entry
+  // in that peer's send run (x_sbase[blk * P + q]); the epilogue stores c' there directly and
+  // k_finalize writes the two slots at every run's end.  x_packed: the gather buffer whose send
+  // runs the last epilogue already wrote (-1: none; the exchange then runs k_pack).
+  bool x_fused = false;
+  pr::DevBuf x_pmask, x_sbase;
+  int x_packed = -1;
 
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
@@ -180,6 +189,7 @@ int group_exchange(pr_graph *const *parts, int n, int buf);
 int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_t mask, const int32_t *rank_of,
                    const int32_t *gpos, DevBuf *cmap);
 int exchange(pr_graph *g, int buf, hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
+double *send_runs(const pr_graph *g, int buf);  // the packed send runs paired with gather buffer buf
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
 }  // namespace pr

@@ -177,6 +177,20 @@ struct SlotPos {
   int n;
   int32_t pos[kMaxParts];
 };
+// Fused pack (pr_graph.h x_fused): where the epilogue stores the contributions the peers read (the
+// send runs of the buffer it writes, peer q's run at soff[q]; P = 0: no fused pack), and where
+// k_finalize stores the two slots that close every peer's run.
+constexpr int kMaxPackParts = 8;
+struct PackDst {
+  double *sbuf;
+  int P, self;
+  int64_t soff[kMaxPackParts];
+};
+struct PackSlots {
+  double *sbuf;
+  int n;
+  int64_t off[kMaxPackParts];
+};
 
 // A class's hot set: for every part p, rows [x*Q_pad, + q_load) of p's slice go to LDS slots
 // 1 + [p*Kp, p*Kp + q_load); slot 0 holds 0.0.  Their gather positions come from a table (the

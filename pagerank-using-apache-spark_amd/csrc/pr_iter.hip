@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
     double *__restrict__ r, const uint32_t *__restrict__ rowinfo, const double *__restrict__ cin,
     double *__restrict__ cout, SlotPos sp, double n_vertices, double teleport,
     double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
-    double *__restrict__ slot_out) {
+    double *__restrict__ slot_out, PackSlots ps) {
   __shared__ double red[kThreads / kWave];
   __shared__ int is_last;
   const int t = threadIdx.x, lane = lane_id();
@@ -101,6 +101,10 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
     slot_out[1] = b;
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (t < ps.n) {  // fused pack: the two slots close every peer's send run
+    ps.sbuf[ps.off[t]] = a;
+    ps.sbuf[ps.off[t] + 1] = b;
+  }
 }
 
 __global__ __launch_bounds__(kThreads) void k_reset(int64_t n_rows, const double *__restrict__ init,
@@ -139,12 +143,18 @@ hipEvent_t next_event(pr_graph *g) {
 int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n_parts, int in_buf,
                     int out_buf) {
   double *cout = g->cbuf[out_buf].as<double>() + g->own_off;
+  PackSlots ps{};
+  if (g->x_fused) {  // the slots of every peer's run (its last two entries)
+    ps.sbuf = send_runs(g, out_buf);
+    for (int q = 0; q < g->nparts; ++q)
+      if (q != g->part) ps.off[ps.n++] = g->x_soff[q + 1] - 2;
+  }
   hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, g->stream, n_long,
                      g->lr_row.as<int32_t>(), g->lr_p0.as<int32_t>(), g->piece_part.as<double>(),
                      parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[in_buf].as<double>(), cout, g->slots, (double)g->V,
                      g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
-                     cout + g->S_pad - 2);
+                     cout + g->S_pad - 2, ps);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
@@ -260,6 +270,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
     PR_HIP(hipStreamSynchronize(s));
   }
   g->cur = 0;
+  g->x_packed = -1;
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
                      dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
@@ -318,11 +329,19 @@ int iter_compute(pr_graph *g) {
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
                          g->partial.as<double>());
     const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
+    PackDst pd{};  // fused pack: c' straight into the send runs paired with buffer `out`
+    if (g->x_fused) {
+      pd.sbuf = send_runs(g, out);
+      pd.P = g->nparts;
+      pd.self = g->part;
+      for (int q = 0; q < g->nparts; ++q) pd.soff[q] = g->x_soff[q];
+    }
     hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
                        g->nblk, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                        g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                        (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
-                       g->eoff.as<int64_t>(), g->epos.as<uint16_t>());
+                       g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
+                       g->x_sbase.as<int32_t>(), pd);
     n_parts += g->ep_blocks;
   }
   PR_HIP(hipGetLastError());
@@ -332,6 +351,7 @@ int iter_compute(pr_graph *g) {
     g->spmv_ev.push_back({base, base + 1});
   }
   PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), n_parts, in, out));
+  g->x_packed = (g->x_fused && g->C > 1) ? out : -1;  // the exchange then skips k_pack
   g->cur = out;
   ++g->iters_done;
   return PR_OK;

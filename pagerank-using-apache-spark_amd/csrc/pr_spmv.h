@@ -760,7 +760,8 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part, const int64_t *__restrict__ eoff,
-    const uint16_t *__restrict__ epos) {
+    const uint16_t *__restrict__ epos, const uint8_t *__restrict__ pmask, const int32_t *__restrict__ sbase,
+    PackDst pd) {
   constexpr int G = kEpiGroup, W = kEpiWin;
   constexpr int NW = NT / kWave;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
@@ -921,12 +922,28 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
       for (int w = 0; w < MW; ++w) any |= mw[w][g];
       if (any == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
       const double rn = affine(Sv, tdc, teleport, damping);
+      double cn = 0.0;
       if (!(info[g] & kRowHole)) {
         r[L] = rn;
         const uint32_t d = info[g] & kRowDegMask;
-        if (d > 0) cout[L] = __ddiv_rn(rn, (double)d);
-        else if (info[g] & kRowSink) dcp = __dadd_rn(dcp, rn);
+        if (d > 0) {
+          cn = __ddiv_rn(rn, (double)d);
+          cout[L] = cn;
+        } else if (info[g] & kRowSink) {
+          dcp = __dadd_rn(dcp, rn);
+        }
         l1p = __dadd_rn(l1p, fabs(rn - rold[g]));
+      }
+      if (pd.P > 1 && g < nb) {  // fused pack: c' into the send run of every peer that reads the row
+        const uint32_t pm = pmask[L];
+        const int64_t sb = (b0 + g) * pd.P;
+        for (int q = 0; q < pd.P; ++q) {
+          const bool has = (pm >> q) & 1u;
+          const unsigned long long bal = __ballot(has);
+          if (bal == 0ull) continue;
+          const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (has) pd.sbuf[pd.soff[q] + sbase[sb + q] + k] = cn;
+        }
       }
     }
   }
@@ -1012,7 +1029,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, con
 // four-wave workgroups
 using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
                           double *, const double *, SlotPos, double, double, double, double2 *, const int64_t *,
-                          const uint16_t *);
+                          const uint16_t *, const uint8_t *, const int32_t *, PackDst);
 template <int C>
 inline EpiGrpFn epi_grp_kernel_c(bool walk, bool narrow) {
   if constexpr (C <= kWave) {

@@ -448,6 +448,37 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode):
             p.close()
 
 
+@pytest.mark.parametrize("P,chunks,narrow", [(2, 0, 0), (3, 1, 0), (8, 0, 1), (8, 1, 0)])
+def test_fused_pack(hip, oracle_c, P, chunks, narrow):
+    """The fused pack (PR_BOPT_PACK_FUSED, the default at P <= 8 with column classes): the split
+    epilogue stores every row's c' straight into the send run of each peer that reads it and
+    k_finalize writes the two slots at every run's end, so the exchange skips k_pack.  Against the
+    oracle and bitwise equal to the same parts packing with k_pack (pack_fused = 0), over a ragged
+    row count (V not a multiple of 64), with whole and chunked runs and both epilogue widths."""
+    rng = np.random.default_rng(90 + P)
+    V = 50003
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.03)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 7)
+    out = {}
+    for fused in (1, 0):
+        opts = {"classes": 16, "pack_fused": fused, "xchg_chunks": chunks, "epi_narrow": narrow}
+        parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split",
+                                   options=opts) for p in range(P)]
+        try:
+            grp = hip.PartGroup(parts)
+            grp.reset()
+            grp.step(3)
+            grp.step(4)
+            grp.sync()
+            out[fused] = grp.ranks()
+        finally:
+            for p in parts:
+                p.close()
+    assert max_rel(out[1], ref["ranks"]) <= RANK_TOL
+    assert np.array_equal(out[1], out[0])
+
+
 @pytest.mark.parametrize("P", [2, 8])
 def test_overlapped_exchange_chunks(hip, oracle_c, P):
     """The overlapped exchange (pr_exchange.hip): with 64 classes the phased k_spmv_hot runs 8
