@@ -216,7 +216,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
                                     g->C == 1 ? 0 : 3, g->gather_est, g->n_walk_groups, g->layout,
-                                    g->hot_cover_ppm, g->C > 1 ? (g->code == pr::kCodeC20 ? 20 : g->code == pr::kCodeC24 ? 24 : 32) : 0};
+                                    g->hot_cover_ppm, g->C > 1 ? (g->code == pr::kCodeC20 || g->code == pr::kCodeC20P ? 20 : g->code == pr::kCodeC24 || g->code == pr::kCodeC24P ? 24 : 32) : 0};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
 }

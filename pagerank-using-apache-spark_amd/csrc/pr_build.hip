@@ -414,6 +414,144 @@ __global__ __launch_bounds__(64) void k_fill_compact(int64_t n_units, const Unit
   atomicAdd(bad, nb);
 }
 
+// Piece codes (pr_internal.h kCodeC20P / kCodeC24P, P > 1): the gather-space range of every
+// (class x, part p) piece -- the positions of part p's class-x sources in this part's gather space
+// (the own region, or the sub-run of p's received run).  lo/hi[x * P + p], hi = 0 when empty.
+__global__ __launch_bounds__(256) void k_piece_bounds(int64_t S_pad, int64_t Q_pad, int C, int P,
+                                                      const int32_t *__restrict__ cmap, int32_t *__restrict__ lo,
+                                                      int32_t *__restrict__ hi) {
+  // one workgroup per (class x, part p) region of the global slices: min / max + 1 of its mapped
+  // positions (a plain reduction: atomics on P*C addresses serialise, 31 ms per s26 part)
+  const int x = (int)(blockIdx.x / P), p = (int)(blockIdx.x % P);
+  const int64_t a0 = (int64_t)p * S_pad + (int64_t)x * Q_pad;
+  int32_t mn = INT32_MAX, mx = 0;
+  for (int64_t o = threadIdx.x; o < Q_pad; o += blockDim.x) {
+    const int64_t a = a0 + o;
+    const int32_t pos = cmap ? cmap[a] : (int32_t)a;
+    if (pos >= 0) {
+      mn = min(mn, pos);
+      mx = max(mx, pos + 1);
+    }
+  }
+  __shared__ int32_t smn[256], smx[256];
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      smn[threadIdx.x] = min(smn[threadIdx.x], smn[threadIdx.x + w]);
+      smx[threadIdx.x] = max(smx[threadIdx.x], smx[threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    lo[blockIdx.x] = smn[0];
+    hi[blockIdx.x] = smx[0];
+  }
+}
+
+// Piece codes: as k_fill_compact, with idx = the hot slot (hotidx) or nh + 1 + the source's index
+// in its class's virtual space (piece table pc[(x * P + p) * 3] = {g0, g1, v0}).  *bad counts the
+// sources outside every piece of the unit's class (none by construction).
+template <int HB, class SideT>
+__global__ __launch_bounds__(64) void k_fill_piece(int64_t n_units, const Unit *__restrict__ units,
+                                                   const int64_t *__restrict__ src_off,
+                                                   const int32_t *__restrict__ n_real,
+                                                   const int32_t *__restrict__ col, const int64_t *__restrict__ ucum,
+                                                   int C, int P, const int32_t *__restrict__ pc,
+                                                   const int32_t *__restrict__ hotidx, int nh,
+                                                   uint16_t *__restrict__ code16, SideT *__restrict__ cside,
+                                                   unsigned long long *n_hot, unsigned long long *bad) {
+  unsigned long long nhot = 0, nb = 0;
+  for (int64_t b = blockIdx.x; b < n_units; b += gridDim.x) {
+    const Unit u = units[b];
+    const int64_t s0 = src_off[b];
+    const int n = n_real[b];
+    int x = 0;
+    while (x + 1 < C && ucum[x + 1] <= b) ++x;  // the unit's class
+    const int32_t *px = pc + (int64_t)x * P * 3;
+    for (int grp = threadIdx.x; grp < u.n / 8; grp += 64) {
+      SideT side = 0;
+      uint32_t lo[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = 8 * grp + j;
+        uint32_t idx = 0;
+        if (i < n) {
+          const int32_t v = col[s0 + i];
+          const int32_t pos = v & 0x7FFFFFFF;
+          const int32_t h = hotidx[pos];
+          if (h) {
+            idx = (uint32_t)h;
+            ++nhot;
+          } else {
+            int p = 0;
+            while (p < P && !(pos >= px[3 * p] && pos < px[3 * p + 1])) ++p;
+            if (p == P) ++nb;
+            else idx = (uint32_t)(nh + 1 + px[3 * p + 2] + (pos - px[3 * p]));
+          }
+          if (u.meta >= 0 && v < 0) side |= (SideT)1 << j;  // segment end (STREAM units)
+        }
+        lo[j] = idx & 0xFFFFu;
+        side |= (SideT)((idx >> 16) & ((1u << HB) - 1u)) << (8 + HB * j);
+      }
+      uint4 q;
+      q.x = lo[0] | lo[1] << 16;
+      q.y = lo[2] | lo[3] << 16;
+      q.z = lo[4] | lo[5] << 16;
+      q.w = lo[6] | lo[7] << 16;
+      *reinterpret_cast<uint4 *>(code16 + (int64_t)u.p8 * 8 + 8 * grp) = q;
+      cside[(int64_t)u.p8 + grp] = side;
+    }
+  }
+  atomicAdd(n_hot, nhot);
+  atomicAdd(bad, nb);
+}
+
+// Host plan of the piece codes: per class the pieces in part order at kPieceAlign-aligned virtual
+// starts; pc = {g0, g1, v0} per (class, part), tbl[x * kPieceTblWords + t] = byte delta
+// 8 * (g0 - v0) of the piece holding virtual block t (0 elsewhere and in the sentinel word
+// kPieceTbl).  vmax = the largest class's virtual extent.
+struct PiecePlan {
+  std::vector<int32_t> pc, tbl;
+  int64_t vmax = 0;
+};
+static int plan_pieces(const pr_graph *g, const int32_t *cmap, int C, int P, PiecePlan *pp, hipStream_t s) {
+  DevBuf lohi;
+  const int64_t np = (int64_t)C * P;
+  PR_TRY(lohi.alloc(sizeof(int32_t) * 2 * (size_t)np));
+  hipLaunchKernelGGL(k_piece_bounds, dim3((unsigned)np), dim3(256), 0, s, g->S_pad, g->Q_pad, C, P, cmap,
+                     lohi.as<int32_t>(), lohi.as<int32_t>() + np);
+  PR_HIP(hipGetLastError());
+  std::vector<int32_t> h((size_t)(2 * np));
+  PR_HIP(hipMemcpyAsync(h.data(), lohi.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s));
+  PR_HIP(hipStreamSynchronize(s));
+  pp->pc.assign((size_t)(3 * np), 0);
+  pp->tbl.assign((size_t)C * kPieceTblWords, 0);
+  pp->vmax = 0;
+  for (int x = 0; x < C; ++x) {
+    int64_t v = 0;
+    for (int p = 0; p < P; ++p) {
+      const int64_t i = (int64_t)x * P + p;
+      const int32_t g0 = h[(size_t)i], g1 = h[(size_t)(np + i)];
+      int32_t *e = &pp->pc[(size_t)(3 * i)];
+      if (g1 <= g0) {  // empty piece: matches nothing
+        e[0] = e[1] = e[2] = 0;
+        continue;
+      }
+      v = (v + kPieceAlign - 1) / kPieceAlign * kPieceAlign;
+      e[0] = g0;
+      e[1] = g1;
+      e[2] = (int32_t)std::min<int64_t>(v, INT32_MAX);
+      for (int64_t t = v >> kPieceShift; t <= (v + (g1 - g0) - 1) >> kPieceShift && t < kPieceTbl; ++t)
+        pp->tbl[(size_t)(x * kPieceTblWords + t)] = (int32_t)(uint32_t)(8u * (uint32_t)(g0 - (int32_t)v));
+      v += g1 - g0;
+    }
+    pp->vmax = std::max(pp->vmax, v);
+  }
+  return PR_OK;
+}
+
 // Column classes of the split layout: the fewest (8, 16, 32, 64) whose class region of the part's
 // gather space (its slice plus the expected received runs at P > 1) fits one XCD's 4 MiB L2 (the
 // phased schedule runs one class per XCD at a time), capped at kAutoMaxClasses; PR_BOPT_CLASSES
@@ -680,7 +818,32 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     pieces = sp.n_pieces;
     if (sp.entries / 8 >= (int64_t(1) << 32)) return fail(PR_ERR_INVALID, "graph part too large for 32-bit unit offsets");
     // LDS hot set per class, then the entry codes
-    const int slots = hot_slots_setting(g->opts);
+    // entry codes: compact when every region index fits (P = 1: a class's sources are its region
+    // of the one slice; 2.5 bytes per entry below 2^19 region rows, 3 below 2^20); a part of a row
+    // partition takes the piece codes when its classes' virtual spaces fit (the hot set then gives
+    // its last kPieceTblSlots slots to the piece table), else 32-bit codes
+    int slots = hot_slots_setting(g->opts);
+    const bool compact = g->opts.codes != 0 && P == 1 && g->gsize == g->S_pad;
+    g->code = compact && g->Q_pad < (int64_t(1) << kC20IdxBits)   ? kCodeC20
+              : compact && g->Q_pad < (int64_t(1) << kC24IdxBits) ? kCodeC24
+                                                                   : kCodeU32;
+    PiecePlan pplan;
+    if (g->opts.codes != 0 && P > 1 && P <= kMaxPackParts) {
+      PR_TRY(plan_pieces(g, cmap.p ? cmap.as<int32_t>() : nullptr, C, P, &pplan, s));
+      HotGeom t{};
+      t.P = P;
+      t.tbl = 1;
+      int ps = slots;
+      for (;; --ps) {  // the largest hot set that leaves LDS room for the table
+        t.Kp = ps / P;
+        if (t.lds_bytes() <= (size_t)kHotLdsBytes) break;
+      }
+      const int64_t top = (int64_t)P * (ps / P) + pplan.vmax;  // largest idx + 1
+      g->code = top < (int64_t(1) << kC20IdxBits)   ? kCodeC20P
+                : top < (int64_t(1) << kC24IdxBits) ? kCodeC24P
+                                                     : kCodeU32;
+      if (code_is_piece(g->code)) slots = ps;
+    }
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
@@ -688,6 +851,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     hg.q_load = (int)std::min<int64_t>(hg.Kp, g->Q_pad);
     hg.S_pad = g->S_pad;
     hg.Q_pad = g->Q_pad;
+    hg.tbl = code_is_piece(g->code) ? 1 : 0;
     g->hot = hg;
     // hot-set gather positions per class, and the LDS slot of every hot gather position
     DevBuf hotidx;
@@ -711,14 +875,17 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->hunits = std::move(sp.units);  // + the empty unit nu
     PR_TRY(g->hucum.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
     PR_TRY(g->poff.alloc(sizeof(int64_t) * (kMaxClasses + 1)));
-    // compact codes when every region index fits (P = 1: a class's sources are its region of the
-    // one slice; a part of a row partition also reads received runs, so it keeps 32-bit codes):
-    // 2.5 bytes per entry below 2^19 region rows, 3 below 2^20
-    const bool compact = g->opts.codes != 0 && P == 1 && g->gsize == g->S_pad;
-    g->code = compact && g->Q_pad < (int64_t(1) << kC20IdxBits)   ? kCodeC20
-              : compact && g->Q_pad < (int64_t(1) << kC24IdxBits) ? kCodeC24
-                                                                   : kCodeU32;
-    const bool c20 = g->code == kCodeC20, c24 = g->code == kCodeC24;
+    const bool c20 = g->code == kCodeC20 || g->code == kCodeC20P, c24 = g->code == kCodeC24 || g->code == kCodeC24P;
+    const bool piece = code_is_piece(g->code);
+    if (piece) {
+      PR_TRY(g->ptab.alloc(sizeof(int32_t) * pplan.tbl.size()));
+      PR_HIP(hipMemcpyAsync(g->ptab.p, pplan.tbl.data(), sizeof(int32_t) * pplan.tbl.size(), hipMemcpyHostToDevice, s));
+    }
+    DevBuf pcd;
+    if (piece) {
+      PR_TRY(pcd.alloc(sizeof(int32_t) * pplan.pc.size()));
+      PR_HIP(hipMemcpyAsync(pcd.p, pplan.pc.data(), sizeof(int32_t) * pplan.pc.size(), hipMemcpyHostToDevice, s));
+    }
     if (c20 || c24) {
       PR_TRY(g->colh.alloc(sizeof(uint16_t) * (sp.entries > 0 ? sp.entries : 8)));
       PR_TRY(g->cside.alloc((c24 ? sizeof(uint64_t) : sizeof(uint32_t)) * (sp.entries > 0 ? sp.entries / 8 : 1)));
@@ -733,7 +900,21 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     if (nu > 0) {
       PR_HIP(hipMemsetAsync(cnt.p, 0, 2 * sizeof(unsigned long long), s));
-      if (c20)
+      const unsigned fgrid = (unsigned)std::min<int64_t>(nu, 65536);
+      const int nhs = P * hg.Kp;
+      if (piece && c20)
+        hipLaunchKernelGGL((k_fill_piece<3, uint32_t>), dim3(fgrid), dim3(64), 0, s, nu, g->hunits.as<Unit>(),
+                           sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
+                           g->hucum.as<int64_t>(), C, P, pcd.as<int32_t>(), hotidx.as<int32_t>(), nhs,
+                           g->colh.as<uint16_t>(), g->cside.as<uint32_t>(), cnt.as<unsigned long long>(),
+                           cnt.as<unsigned long long>() + 1);
+      else if (piece)
+        hipLaunchKernelGGL((k_fill_piece<4, uint64_t>), dim3(fgrid), dim3(64), 0, s, nu, g->hunits.as<Unit>(),
+                           sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(), g->col.as<int32_t>(),
+                           g->hucum.as<int64_t>(), C, P, pcd.as<int32_t>(), hotidx.as<int32_t>(), nhs,
+                           g->colh.as<uint16_t>(), g->cside.as<uint64_t>(), cnt.as<unsigned long long>(),
+                           cnt.as<unsigned long long>() + 1);
+      else if (c20)
         hipLaunchKernelGGL((k_fill_compact<3, uint32_t>), dim3((unsigned)std::min<int64_t>(nu, 65536)), dim3(64), 0, s,
                            nu, g->hunits.as<Unit>(), sp.src_off.as<int64_t>(), sp.n_real.as<int32_t>(),
                            g->col.as<int32_t>(), g->Q_pad, hg.q_load, g->colh.as<uint16_t>(),
@@ -752,7 +933,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
       unsigned long long n_hot[2] = {0, 0};
       PR_HIP(hipMemcpyAsync(n_hot, cnt.p, sizeof(n_hot), hipMemcpyDeviceToHost, s));
       PR_HIP(hipStreamSynchronize(s));
-      if (n_hot[1]) return fail(PR_ERR_STATE, "compact codes: a unit reads outside its class region");
+      if (n_hot[1]) return fail(PR_ERR_STATE, "compact codes: a unit reads outside its class region / pieces");
       g->hot_cover_ppm = lm > 0 ? (int64_t)((double)n_hot[0] * 1e6 / (double)lm) : 0;
     }
     g->n_segs = sp.n_long;

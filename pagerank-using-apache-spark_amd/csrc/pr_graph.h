@@ -84,6 +84,7 @@ struct pr_graph {
   // index bits, cside = one u32 of end marks and high bits per 8 entries)
   int code = pr::kCodeU32;
   pr::DevBuf cside;
+  pr::DevBuf ptab;  // piece codes (kCodeC20P / kCodeC24P): per class kPieceTblWords gather deltas
   int ep_blocks = 0;
   pr::ClassGeom geo{};
   pr::HotGeom hot{};

@@ -148,13 +148,30 @@ constexpr uint32_t kEntZero = 0u;  // LDS slot 0
 // -> 2.5 B per in-link, idx < 2^19 (R-MAT s26: Q_pad = 512640).  Class regions up to 2^20 rows
 // (the Twitter shape: Q_pad = 650816) take the 3-byte variant kCodeC24: a u64 side word per lane,
 // bits 0-7 the end marks, bits 8 + 4j .. 11 + 4j the high 4 bits of idx (one 8-byte load).  Larger
-// class regions, and parts of a row partition (whose class sources span several received runs),
-// keep the 32-bit codes.
+// class regions keep the 32-bit codes.
+//
+// Parts of a row partition (P > 1): a class's sources are its region of the own slice plus, for
+// every peer, the sub-run of that peer's received run holding the peer's class-x sources (a run is
+// sorted by the peer's slice position, so that sub-run is contiguous in the gather space).  The
+// *piece* codes kCodeC20P / kCodeC24P (same streams as kCodeC20 / kCodeC24) index a per-class
+// virtual space: idx 1..P*Kp = LDS hot slot (as the 32-bit codes' hot entries), idx = P*Kp + 1 + k
+// a cold source at virtual index k, where the class's pieces (in part order) start at multiples of
+// kPieceAlign.  Gather position = k + tbl[x][k / kPieceAlign]: a per-class table of kPieceTbl
+// deltas (plus a 0 sentinel that keeps hot entries' loads out of range), restaged into LDS with
+// the hot set.  The hot set gives up kPieceTblSlots slots for it.
 constexpr int kCodeU32 = 0;
 constexpr int kCodeC20 = 1;
 constexpr int kCodeC24 = 2;
+constexpr int kCodeC20P = 3;
+constexpr int kCodeC24P = 4;
 constexpr int kC20IdxBits = 19;
 constexpr int kC24IdxBits = 20;
+constexpr int kPieceShift = 12;
+constexpr int kPieceAlign = 1 << kPieceShift;
+constexpr int kPieceTbl = (1 << kC24IdxBits) >> kPieceShift;  // 256 blocks cover any 20-bit index
+constexpr int kPieceTblWords = kPieceTbl + 2;                 // + the sentinel, rounded to 8 bytes
+constexpr int kPieceTblSlots = kPieceTblWords / 2;            // in doubles
+constexpr __host__ __device__ bool code_is_piece(int code) { return code >= kCodeC20P; }
 // LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part), one
 // more 0.0 slot (where compact cold entries point their LDS read), the workgroup's unit counter,
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
@@ -198,14 +215,16 @@ struct PackSlots {
 struct HotGeom {
   int C, P, Kp, q_load;
   int64_t S_pad, Q_pad;
+  int tbl;  // 1: piece codes, the class's piece table follows the staging windows (kPieceTblSlots)
   __host__ __device__ int slots() const { return P * Kp + 1; }
   // slot `slots()` holds 0.0 (compact codes' cold entries read it), slot `slots() + 1` is a
   // control word (the workgroup's unit counter, pr_spmv.h hot_class_units); the staging windows
   // start 16-byte aligned after it
   __host__ __device__ int ctr_slot() const { return slots() + 1; }
   __host__ __device__ int stage_off() const { return (slots() + 3) & ~1; }
+  __host__ __device__ int tbl_off() const { return stage_off() + (kHotThreads / 64) * kStageSlots; }
   __host__ __device__ size_t lds_bytes() const {
-    return sizeof(double) * ((size_t)stage_off() + (size_t)(kHotThreads / 64) * kStageSlots);
+    return sizeof(double) * ((size_t)tbl_off() + (tbl ? (size_t)kPieceTblSlots : 0));
   }
 };
 

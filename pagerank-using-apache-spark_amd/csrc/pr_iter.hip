@@ -171,7 +171,9 @@ int prepare_hot_kernel() {
       }
   for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
                         reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>)})
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P>)})
     PR_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   return PR_OK;
 }
@@ -237,13 +239,15 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   if (ph1 < 0) ph1 = n_hot_phases(g);
   const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
-  auto kern = g->code == kCodeC20   ? k_spmv_hot<kCodeC20>
-              : g->code == kCodeC24 ? k_spmv_hot<kCodeC24>
-                                    : k_spmv_hot<kCodeU32>;
+  auto kern = g->code == kCodeC20    ? k_spmv_hot<kCodeC20>
+              : g->code == kCodeC24  ? k_spmv_hot<kCodeC24>
+              : g->code == kCodeC20P ? k_spmv_hot<kCodeC20P>
+              : g->code == kCodeC24P ? k_spmv_hot<kCodeC24P>
+                                     : k_spmv_hot<kCodeU32>;
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),
-                     g->piece_part.as<double>(), g->hpos.as<int32_t>(), ph0, ph1);
+                     g->piece_part.as<double>(), g->hpos.as<int32_t>(), g->ptab.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }

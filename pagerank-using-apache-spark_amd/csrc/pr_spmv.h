@@ -402,10 +402,22 @@ __device__ __forceinline__ LaneMeta derive_meta(uint32_t endm) {
 struct ClassSrc {
   __amdgpu_buffer_rsrc_t crs;
   uint32_t zb, hb;
+  const uint32_t *tbl;  // piece codes: the class's piece table in LDS (pr_internal.h kCodeC20P)
 };
+
+// Byte offset of a compact code's cold source: past the class's hot positions (hot and padding
+// entries wrap to >= 2^31: out of range); piece codes add their virtual block's delta (hot entries
+// read the 0 sentinel and stay out of range).
+template <bool PIECE>
+__device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs) {
+  uint32_t go = b8 - cs.hb;
+  if constexpr (PIECE) go += cs.tbl[min(go >> (kPieceShift + 3), (uint32_t)kPieceTbl)];
+  return go;
+}
 
 // The unit's values: per entry an LDS read (hot) and a range-checked gather-space load (cold),
 // one of them an exact 0.
+template <bool PIECE>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const double *hot, const ClassSrc &cs,
                                                  double (&v)[kWavePT]) {
 #pragma unroll
@@ -418,6 +430,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
     v[j] = __dadd_rn(a, b);
   }
 }
+template <bool PIECE>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const double *hot, const ClassSrc &cs,
                                                  double (&v)[kWavePT]) {
 #pragma unroll
@@ -427,11 +440,12 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, b8 - cs.hb, 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, 0));
     v[j] = __dadd_rn(a, b);
   }
 }
 
+template <bool PIECE>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const double *hot, const ClassSrc &cs,
                                                  double (&v)[kWavePT]) {
 #pragma unroll
@@ -441,7 +455,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, b8 - cs.hb, 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, 0));
     v[j] = __dadd_rn(a, b);
   }
 }
@@ -545,10 +559,19 @@ template <>
 struct CodeOf<kCodeC24> {
   using T = WaveCodesC24;
 };
+template <>
+struct CodeOf<kCodeC20P> {
+  using T = WaveCodesC20;
+};
+template <>
+struct CodeOf<kCodeC24P> {
+  using T = WaveCodesC24;
+};
 template <int CODE>
 __device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typename CodeOf<CODE>::T &w) {
-  if constexpr (CODE == kCodeC20) wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), cd.side, w);
-  else if constexpr (CODE == kCodeC24)
+  if constexpr (CODE == kCodeC20 || CODE == kCodeC20P)
+    wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), cd.side, w);
+  else if constexpr (CODE == kCodeC24 || CODE == kCodeC24P)
     wave_unit_codes(u, static_cast<const uint16_t *>(cd.codes), reinterpret_cast<const uint64_t *>(cd.side), w);
   else wave_unit_codes(u, static_cast<const uint32_t *>(cd.codes), w);
 }
@@ -599,7 +622,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   unit_codes<CODE>(u[0], cd, wc[0]);
   u[1] = unit_at(k1 < end ? k1 : none_k);
   unit_codes<CODE>(u[1], cd, wc[1]);
-  wave_unit_gather(wc[0], hot, cs, v[0]);
+  wave_unit_gather<code_is_piece(CODE)>(wc[0], hot, cs, v[0]);
   while (true) {
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl) {
@@ -610,7 +633,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/)
       wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
-      wave_unit_gather(wc[s1], hot, cs, v[s1]);
+      wave_unit_gather<code_is_piece(CODE)>(wc[s1], hot, cs, v[s1]);
       k = k1;
       k1 = k2;
       if (k >= end) return;
@@ -630,19 +653,24 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           uint32_t cin_bytes, double *__restrict__ partial,
                                                           const int64_t *__restrict__ poff,
                                                           double *__restrict__ piece_part,
-                                                          const int32_t *__restrict__ hpos, int ph0, int ph1) {
+                                                          const int32_t *__restrict__ hpos,
+                                                          const int32_t *__restrict__ ptab, int ph0, int ph1) {
   extern __shared__ double hot[];
   const int nh = hg.P * hg.Kp;
+  constexpr bool kPiece = code_is_piece(CODE);
   ClassSrc cs;
   cs.zb = (uint32_t)hg.slots() * 8u;
-  cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
-  if constexpr (CODE == kCodeU32) cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
+  cs.hb = kPiece ? cs.zb : (uint32_t)(hg.q_load + 1) * 8u;  // piece codes: cold idx = nh + 1 + k
+  uint32_t *tblw = reinterpret_cast<uint32_t *>(hot + hg.tbl_off());
+  cs.tbl = tblw;
+  if constexpr (CODE == kCodeU32 || kPiece)
+    cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)cin, 0, cin_bytes, 0x00020000);
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;  // this wave's staging window
   const int team = (int)(blockIdx.x / kXcds), nteams = (int)(gridDim.x / kXcds);
   for (int ph = ph0; ph < ph1; ++ph) {
     const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
-    if constexpr (CODE != kCodeU32) {  // region index q_load + 1 + k -> position x*Q_pad + q_load + k
+    if constexpr (CODE == kCodeC20 || CODE == kCodeC24) {  // region index q_load + 1 + k -> x*Q_pad + q_load + k
       const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;
       cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0,
                                                  (uint32_t)((hg.Q_pad - hg.q_load) * 8), 0x00020000);
@@ -669,6 +697,9 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
         if (i < nh) hot[1 + i] = val[j];
       }
     }
+    if constexpr (kPiece)
+      for (int i = (int)threadIdx.x; i < kPieceTblWords; i += kHotThreads)
+        tblw[i] = (uint32_t)ptab[(int64_t)x * kPieceTblWords + i];
     if (threadIdx.x == 0) {
       hot[0] = 0.0;
       hot[hg.slots()] = 0.0;

@@ -599,7 +599,8 @@ def test_compact_codes_bitwise(hip, oracle_c, classes, slots):
     indices with end marks and high bits in a side word per 8 entries.  Same entries, same sums
     in the same order as the 32-bit codes, so the ranks are bitwise equal; with no hot set, a
     partial one and the default one (every class region fully hot here), with hub segments in
-    pieces and empty (row, class) pairs.  Parts of a row partition keep the 32-bit codes."""
+    pieces and empty (row, class) pairs.  Parts of a row partition take the piece codes
+    (test_piece_codes_bitwise)."""
     opts = {"classes": classes, "hot_slots": slots}
     rng = np.random.default_rng(300 + classes + slots)
     V = 60000
@@ -616,7 +617,67 @@ def test_compact_codes_bitwise(hip, oracle_c, classes, slots):
     assert [s.dangling_sum for s in st32] == [s.dangling_sum for s in stats]
     with hip.PageRankGraph(V, src, dst, part=0, n_parts=2, keep_canonical=False, layout="split",
                            options=opts) as g:
-        assert g.info()["code_bits"] == 32
+        assert g.info()["code_bits"] == 20
+
+
+def _group_ranks(hip, V, src, dst, P, opts, iters):
+    parts = [hip.PageRankGraph(V, src, dst, part=p, n_parts=P, keep_canonical=False, layout="split",
+                               options=opts) for p in range(P)]
+    try:
+        infos = [p.info() for p in parts]
+        grp = hip.PartGroup(parts)
+        grp.reset()
+        grp.step(iters // 2)
+        grp.step(iters - iters // 2)
+        grp.sync()
+        return grp.ranks(), infos
+    finally:
+        for p in parts:
+            p.close()
+
+
+@pytest.mark.parametrize("P,classes,slots,xmode,chunks", [
+    (2, 16, -1, "sparse", 0), (3, 32, 300, "sparse", 1), (8, 64, -1, "sparse", 1),
+    (8, 16, 0, "sparse", 0), (4, 32, -1, "allgather", 0)])
+def test_piece_codes_bitwise(hip, oracle_c, P, classes, slots, xmode, chunks):
+    """Piece codes for the parts of a row partition (pr_internal.h kCodeC20P): a class's sources
+    are the own region plus one sub-run of every peer's received run (or every slice's region with
+    the whole-slice all-gather); the codes index a per-class virtual space whose 4096-aligned blocks
+    map back to gather positions through an LDS table.  Same entries and sums as the 32-bit codes
+    (PR_BOPT_CODES = 0), so the ranks are bitwise equal; with and without a hot set, with chunked
+    runs, and against the oracle."""
+    rng = np.random.default_rng(500 + P + classes)
+    V = 50003
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.03)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 7)
+    opts = {"classes": classes, "hot_slots": slots, "xchg_chunks": chunks,
+            "exchange_allgather": int(xmode == "allgather")}
+    r, infos = _group_ranks(hip, V, src, dst, P, opts, 7)
+    assert all(i["code_bits"] == 20 and i["classes"] == classes for i in infos)
+    if slots == -1:  # the piece table takes its LDS from the hot set
+        assert all(0 < i["hot_slots"] < 18429 for i in infos)
+    r32, infos32 = _group_ranks(hip, V, src, dst, P, dict(opts, codes=0), 7)
+    assert all(i["code_bits"] == 32 for i in infos32)
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+    assert np.array_equal(r, r32)
+
+
+def test_piece_codes_widen(hip, oracle_c):
+    """A part whose class virtual space passes 2^19 (8 classes over 4.4 M vertices at P = 2:
+    own regions of 275 K rows plus ~254 K received sources per class) takes the 3-byte piece codes
+    (kCodeC24P), bitwise the ranks of the 32-bit codes, and matches the oracle."""
+    rng = np.random.default_rng(78)
+    V = 4400000
+    src, dst = random_edges(rng, V, 24000000, hub_frac=0.01)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 4)
+    opts = {"classes": 8}
+    r, infos = _group_ranks(hip, V, src, dst, 2, opts, 4)
+    assert all(i["code_bits"] == 24 for i in infos)
+    r32, _ = _group_ranks(hip, V, src, dst, 2, dict(opts, codes=0), 4)
+    assert max_rel(r, ref["ranks"]) <= RANK_TOL
+    assert np.array_equal(r, r32)
 
 
 @pytest.mark.parametrize("V,bits", [(4400000, 24), (8800000, 32)])
