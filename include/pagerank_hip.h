@@ -75,7 +75,7 @@ extern "C" {
 #define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
 #define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots)          */
 #define PR_INFO_HOT_COVER 22   /* in-links read from the LDS hot sets, parts per million      */
-#define PR_INFO_CODE_BITS 23   /* bits per in-link of the split layout's entry codes: 20 compact, 32 */
+#define PR_INFO_CODE_BITS 23   /* bits per in-link of the split layout's entry codes: 20 / 24 compact, 32 */
 #define PR_INFO_COUNT 24
 
 /* ---- pr_get_stats indices ------------------------------------------------------------- */
@@ -130,8 +130,9 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_EPI_WALK 6    /* split layout: 1 (default) per-row walk of sparse epilogue groups, 0 never */
 #define PR_BOPT_EPI_NARROW 7  /* split layout: -1 auto (default), 0 four-wave, 1 one-wave epilogue workgroups */
 #define PR_BOPT_CODES 8       /* split layout: -1 (default) compact entry codes where they fit (P = 1: 2.5 bytes
-                                 for class regions < 2^19 positions, 3 bytes < 2^20), 0 always 4-byte codes;
-                                 same sums either way (PR_INFO code_bits: 20 / 24 / 32) */
+                                 for class regions < 2^19 positions, 3 bytes < 2^20; P = 2..8: piece codes,
+                                 2.5 / 3 bytes when hot slots + a class's pieces < 2^19 / 2^20), 0 always
+                                 4-byte codes; same sums either way (PR_INFO code_bits: 20 / 24 / 32) */
 #define PR_BOPT_PACK_FUSED 9  /* P > 1 (per-peer runs, split layout): 1 (default) the epilogue writes the
                                  contributions every peer reads straight into the send runs, 0 a separate
                                  pack kernel gathers them after the pass; same values either way */

@@ -81,7 +81,8 @@ struct pr_graph {
   pr::DevBuf colh, hunits, hucum, poff, partial, rmask, cbase, seg_slot, seg_p0, hpos;
   // entry code format (pr_internal.h): kCodeU32 (colh = u32 codes), kCodeC24 (as C20 with a u64
   // side word and 4 high bits per entry) or kCodeC20 (colh = u16 low
-  // index bits, cside = one u32 of end marks and high bits per 8 entries)
+  // index bits, cside = one u32 of end marks and high bits per 8 entries); kCodeC20P / kCodeC24P
+  // at P > 1 (the same streams, indices into a class's pieces; ptab maps them back)
   int code = pr::kCodeU32;
   pr::DevBuf cside;
   pr::DevBuf ptab;  // piece codes (kCodeC20P / kCodeC24P): per class kPieceTblWords gather deltas
