@@ -24,6 +24,8 @@ def main():
     import sparky_hip
 
     ap = argparse.ArgumentParser()
+    ap.add_argument("--graph", choices=["rmat", "er", "lj", "twitter"], default="rmat",
+                    help="workload of bench.py (sparky_hip.workloads); rmat keeps this tool's seed 1")
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--parts", default="2,4,8")
@@ -32,11 +34,16 @@ def main():
     ap.add_argument("--build-option", action="append", default=[], metavar="NAME=VALUE",
                     help="pr_graph_create_ex option of every part (P > 1), e.g. hot_slots=9000; repeatable")
     a = ap.parse_args()
-    E = a.edge_factor << a.scale
-    s = torch.empty(E, dtype=torch.int32, device="cuda")
-    d = torch.empty(E, dtype=torch.int32, device="cuda")
-    sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=1)
-    V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    if a.graph == "rmat":
+        E = a.edge_factor << a.scale
+        s = torch.empty(E, dtype=torch.int32, device="cuda")
+        d = torch.empty(E, dtype=torch.int32, device="cuda")
+        sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=1)
+        V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
+    else:
+        from sparky_hip.workloads import generate
+        wl = generate(a.graph, scale=a.scale, edge_factor=a.edge_factor, device=0)
+        V, E, s, d = wl.n_vertices, wl.n_edges, wl.src, wl.dst
     torch.cuda.synchronize()
 
     def run(P):
@@ -75,15 +82,16 @@ def main():
                 p.close()
 
     r1, ms1, _ = run(1)
-    print(json.dumps({"scale": a.scale, "V": V, "parts": 1, "ms_per_iter": round(ms1, 3)}), flush=True)
+    print(json.dumps({"graph": a.graph, "scale": a.scale, "V": V, "parts": 1, "ms_per_iter": round(ms1, 3)}), flush=True)
     for P in [int(x) for x in a.parts.split(",")]:
         r, ms, infos = run(P)
         rel = float(np.max(np.abs(r - r1) / np.abs(r1)))
         send = [i["xchg_send"] for i in infos]
         recv = [i["xchg_recv"] for i in infos]
         whole = [(P - 1) * (i["local_rows"] + 2) for i in infos]
-        print(json.dumps({"scale": a.scale, "parts": P, "mode": "allgather" if a.allgather else "sparse",
+        print(json.dumps({"graph": a.graph, "scale": a.scale, "parts": P, "mode": "allgather" if a.allgather else "sparse",
                           "ms_per_iter_all_parts_one_gpu": round(ms, 3), "max_rel_vs_1part": rel,
+                          "code_bits": [i["code_bits"] for i in infos], "classes": [i["classes"] for i in infos],
                           "xchg_recv_doubles": recv, "xchg_send_doubles": send,
                           "recv_frac_of_allgather": round(sum(recv) / max(sum(whole), 1), 4)}), flush=True)
         assert rel <= 1e-11, rel
