@@ -83,7 +83,7 @@ def main():
 
     r1, ms1, _ = run(1)
     print(json.dumps({"graph": a.graph, "scale": a.scale, "V": V, "parts": 1, "ms_per_iter": round(ms1, 3)}), flush=True)
-    for P in [int(x) for x in a.parts.split(",")]:
+    for P in [int(x) for x in a.parts.replace("+", ",").split(",")]:  # "+" too (tools/gpu/run.sh eats commas)
         r, ms, infos = run(P)
         rel = float(np.max(np.abs(r - r1) / np.abs(r1)))
         send = [i["xchg_send"] for i in infos]
