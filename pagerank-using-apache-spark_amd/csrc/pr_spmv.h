@@ -460,41 +460,6 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const do
   }
 }
 
-#ifndef PR_PIECE_HOIST  // A/B builds only (tools/ab_build.sh -DPR_PIECE_HOIST=0): lookups at the gather issue
-#define PR_PIECE_HOIST 1
-#endif
-// Piece codes: the table deltas of a unit's entries, read before the previous unit's reduce so
-// the LDS latency hides behind it (a lookup between the codes and the gather issue would delay
-// every gather); hot and padding entries read the 0 sentinel.
-__device__ __forceinline__ uint32_t entry_idx(const WaveCodesC20 &w, int j) {
-  const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
-  return lo | (((w.s >> (8 + 3 * j)) & 7u) << 16);
-}
-__device__ __forceinline__ uint32_t entry_idx(const WaveCodesC24 &w, int j) {
-  const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
-  return lo | ((uint32_t)(w.s >> (8 + 4 * j)) & 15u) << 16;
-}
-template <class WC>
-__device__ __forceinline__ void piece_deltas(const WC &w, const ClassSrc &cs, uint32_t (&d)[kWavePT]) {
-#pragma unroll
-  for (int j = 0; j < kWavePT; ++j) {
-    const uint32_t go = (entry_idx(w, j) << 3) - cs.hb;
-    d[j] = cs.tbl[min(go >> (kPieceShift + 3), (uint32_t)kPieceTbl)];
-  }
-}
-template <class WC>
-__device__ __forceinline__ void wave_unit_gather_pieces(const WC &w, const uint32_t (&d)[kWavePT], const double *hot,
-                                                        const ClassSrc &cs, double (&v)[kWavePT]) {
-#pragma unroll
-  for (int j = 0; j < kWavePT; ++j) {
-    const uint32_t b8 = entry_idx(w, j) << 3;
-    const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
-    const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, b8 - cs.hb + d[j], 0, 0));
-    v[j] = __dadd_rn(a, b);
-  }
-}
-
 // Per-lane sums along the segment ends, then the wave's segmented scan; on return sv[j] is the
 // lane's running sum at entry j (restarted after every end) and *carry the sum flowing into the
 // lane's first segment from earlier lanes.
@@ -667,15 +632,10 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       unit_codes<CODE>(u[s2], cd, wc[s2]);
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/)
-      if constexpr (code_is_piece(CODE) && PR_PIECE_HOIST) {
-        uint32_t d[kWavePT];
-        piece_deltas(wc[s1], cs, d);
-        wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
-        wave_unit_gather_pieces(wc[s1], d, hot, cs, v[s1]);
-      } else {
-        wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
-        wave_unit_gather<code_is_piece(CODE)>(wc[s1], hot, cs, v[s1]);
-      }
+      wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+      // piece codes look their table delta up here; reading them before the reduce instead
+      // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
+      wave_unit_gather<code_is_piece(CODE)>(wc[s1], hot, cs, v[s1]);
       k = k1;
       k1 = k2;
       if (k >= end) return;
