@@ -420,6 +420,8 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
     }
     for (int p = 0; p < n; ++p) PR_HIP(hipStreamWaitEvent(g->xstream, parts[p]->x_pack_ev, 0));
     const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
+    // copy engines (PR_BOPT_XCHG_SDMA): no CU is taken from the receiver's k_spmv_hot phases
+    const hipMemcpyKind kind = g->opts.xchg_sdma ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
     for (int c = 0; c < steps; ++c) {
       const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;  // unchunked: whole runs
       for (int p = 0; p < n; ++p) {
@@ -430,8 +432,8 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
         if (r1 - r0 != s1 - s0) return fail(PR_ERR_STATE, "exchange lists disagree");
         if (r1 > r0)
           PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + g->S_pad + g->x_roff[p] + r0,
-                                send_runs(src, buf) + src->x_soff[q] + s0, sizeof(double) * (r1 - r0),
-                                hipMemcpyDeviceToDevice, g->xstream));
+                                send_runs(src, buf) + src->x_soff[q] + s0, sizeof(double) * (r1 - r0), kind,
+                                g->xstream));
       }
       PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
     }

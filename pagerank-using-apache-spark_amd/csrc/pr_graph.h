@@ -42,6 +42,7 @@ struct pr_build_opts {
   int epi_narrow = -1;   // -1: by the share of walking groups
   int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
   bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
+  bool xchg_sdma = false;  // group path: runs move on the copy engines (hipMemcpyDeviceToDeviceNoCU)
 };
 
 struct pr_graph {

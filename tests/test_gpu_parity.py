@@ -663,6 +663,23 @@ def test_piece_codes_bitwise(hip, oracle_c, P, classes, slots, xmode, chunks):
     assert np.array_equal(r, r32)
 
 
+@pytest.mark.parametrize("P,chunks", [(2, 1), (3, 0), (8, 1)])
+def test_group_exchange_copy_engines(hip, oracle_c, P, chunks):
+    """PR_BOPT_XCHG_SDMA: the group path moves the runs on the copy engines
+    (hipMemcpyDeviceToDeviceNoCU) instead of blit kernels; the same doubles land in the same
+    places, so the ranks are bitwise those of the device copies, with whole and chunked runs."""
+    rng = np.random.default_rng(700 + P)
+    V = 50003
+    src, dst = random_edges(rng, V, 600000, hub_frac=0.03)
+    csr = oracle_c.build_csr(V, src, dst)
+    ref = oracle_c.run(csr, 7)
+    opts = {"classes": 16, "xchg_chunks": chunks}
+    r_sdma, _ = _group_ranks(hip, V, src, dst, P, dict(opts, xchg_sdma=1), 7)
+    r_blit, _ = _group_ranks(hip, V, src, dst, P, opts, 7)
+    assert max_rel(r_sdma, ref["ranks"]) <= RANK_TOL
+    assert np.array_equal(r_sdma, r_blit)
+
+
 def test_piece_codes_widen(hip, oracle_c):
     """A part whose class virtual space passes 2^19 (8 classes over 4.4 M vertices at P = 2:
     own regions of 275 K rows plus ~254 K received sources per class) takes the 3-byte piece codes
