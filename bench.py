@@ -5,9 +5,13 @@
 A step is one PageRank iteration (Sparky.java:189-235) over the whole graph, inputs resident
 in HBM.  The graph is generated on the GPU (sparky_hip.workloads: seeded R-MAT, Graph500
 a/b/c = .57/.19/.19, edge factor 16), interned in first-appearance order (pr_intern_device) and
-built by libpagerank_hip; none of that is timed.  N > 1: launched by torch.distributed.run, one
-process per GPU; every rank builds its row part of the same graph and the parts exchange the
-contributions each one reads with grouped RCCL send/recv per iteration (inside the library).
+built by libpagerank_hip; none of that is timed.  N > 1: one process per GPU under
+torch.distributed.run -- the driver's launcher, or, for a plain `python bench.py --gpus N`, a
+torch.distributed.run child this process starts before touching any GPU (its rank-0 line is
+relayed; a WORLD_SIZE that disagrees with --gpus, or fewer GPUs than ranks, ends with an "error"
+line and a non-zero status instead of a mislabelled number); every rank builds its row part of
+the same graph and the parts exchange the contributions each one reads with grouped RCCL
+send/recv per iteration (inside the library).
 value = E' (distinct edges of the whole graph) / (max-over-ranks time per step) / 1e9.
 
 Rank 0 prints ONE JSON line (the driver's contract), including
@@ -80,11 +84,8 @@ class Watchdog:
             self._stage = None
 
     def error_line(self, stage: str, limit: float) -> dict:
-        return {"metric": METRIC, "value": None, "unit": "GTEPS", "n_gpus": self.world, "steps": self.steps,
-                "warmup": self.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
-                "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded device-side generator; no dataset)",
-                "config": {"workload": None}, "roofline": None, "cpu_baseline": None,
-                "error": f"stage '{stage}' exceeded its {limit:.0f} s deadline on rank {self.rank} (hang?)"}
+        return contract_error_line(self.world, self.steps, self.warmup,
+                                   f"stage '{stage}' exceeded its {limit:.0f} s deadline on rank {self.rank} (hang?)")
 
     def _watch(self) -> None:
         while True:
@@ -120,6 +121,41 @@ def pmc_traffic(workload: str):
     except Exception:
         return None
     return None
+
+
+def gather_rates():
+    """Measured service rates of the pass's two value sources (tools/diag_rates.py on MI355X,
+    committed as profiles/rates.json): random 8-byte gathers from an L2-resident table, and random
+    8-byte LDS reads with one 1024-thread workgroup per CU.  None when absent."""
+    path = os.path.join(ROOT, "profiles", "rates.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return {"l2_gather_per_s": d["gather_2MiB_per_s"], "lds_read_per_s": d["lds_reads_256wg_per_s"],
+                "source": "profiles/rates.json (tools/diag_rates.py)"}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def gather_roofline(info: dict, spmv_ms: float):
+    """roofline.gather: the pass's in-link values come from the class's LDS hot
+    set (hot_cover of the in-links) or as divergent 8-byte gathers of the gather space that hit the
+    XCD's L2 (the class phases keep one class region resident).  Each source has its own service
+    rate; a pass cannot run faster than the slower of the two floors, whatever its HBM bytes."""
+    rates = gather_rates()
+    if rates is None or spmv_ms <= 0:
+        return None
+    e = info["local_edges"]
+    cover = info.get("hot_cover_ppm", 0) / 1e6
+    cold, lds = e * (1.0 - cover), e * cover
+    t_cold = cold / rates["l2_gather_per_s"] * 1e3
+    t_lds = lds / rates["lds_read_per_s"] * 1e3
+    return {"cold_gathers": int(cold), "lds_entries": int(lds),
+            "l2_gather_rate_G_per_s": round(rates["l2_gather_per_s"] / 1e9, 1),
+            "lds_read_rate_G_per_s": round(rates["lds_read_per_s"] / 1e9, 1),
+            "cold_floor_ms": round(t_cold, 4), "lds_floor_ms": round(t_lds, 4),
+            "frac_cold": round(t_cold / spmv_ms, 4), "frac_lds": round(t_lds / spmv_ms, 4),
+            "rates_from": rates["source"]}
 
 
 def host_cores():
@@ -173,6 +209,53 @@ def oracle_leg(g, V: int, iters: int, pick_threads: bool):
     return res, threads, desc, csr.n_edges
 
 
+def contract_error_line(world: int, steps: int, warmup: int, msg: str) -> dict:
+    """The contract's JSON line for a run that measured nothing ("value": null, "error")."""
+    return {"metric": METRIC, "value": None, "unit": "GTEPS", "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": None, "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded device-side generator; no dataset)", "config": {"workload": None},
+            "roofline": None, "cpu_baseline": None, "error": msg}
+
+
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` (N > 1) outside a launcher: start N ranks under
+    torch.distributed.run as a CHILD process (this parent never imports torch or touches a GPU, and
+    never execs), relay its stdout -- rank 0's JSON line -- and exit with its status.  A child that
+    ends without a JSON line gets one with "error" from here, so the driver never reads a 1-GPU
+    number for an N-GPU request."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log(f"--gpus {a.gpus} without a launcher: starting {a.gpus} ranks (torch.distributed.run, port {port})")
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+
+    def forward(signum, _frame):  # the driver's SIGTERM / ^C reach the ranks through torchrun
+        child.send_signal(signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    seen = False
+    for line in child.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.lstrip().startswith("{") and '"metric"' in line:
+            seen = True
+    rc = child.wait()
+    if not seen:
+        print(json.dumps(contract_error_line(a.gpus, a.steps, a.warmup,
+                                             f"{a.gpus}-rank launch ended with status {rc} and no result line")),
+              flush=True)
+        return rc if rc != 0 else 4
+    return rc
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,10 +288,20 @@ def main() -> int:
                     help="N > 1: ranks generate and build their parts one after another (with --share-device: "
                          "one edge list on the device at a time)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:  # a launcher with a different rank count: measure nothing rather than mislabel
+        msg = f"WORLD_SIZE={world} but --gpus={a.gpus}: the launcher and the request disagree"
+        log(msg)
+        if rank == 0:
+            print(json.dumps(contract_error_line(a.gpus, a.steps, a.warmup, msg)), flush=True)
+        return 2
     limits = {"init": 300, "generate": 300, "build": 600, "attach": 180, "calibration": 600, "timed": 600, "parity": 900}
     if a.stage_timeout is not None:
         limits = {k: a.stage_timeout for k in limits}
@@ -224,8 +317,15 @@ def main() -> int:
     import sparky_hip
     from sparky_hip.workloads import generate
 
-    if world != a.gpus:
-        log(f"WORLD_SIZE={world} but --gpus={a.gpus}; using WORLD_SIZE")
+    n_dev = torch.cuda.device_count()  # counts without initialising the GPU
+    need = 1 if a.share_device else world
+    if n_dev < need:
+        msg = (f"{n_dev} GPU(s) visible, {need} needed for {world} rank(s)"
+               + ("" if a.share_device or n_dev == 0 else " (--share-device rehearses N ranks on fewer GPUs)"))
+        log(msg)
+        if rank == 0:
+            print(json.dumps(contract_error_line(world, a.steps, a.warmup, msg)), flush=True)
+        return 2
     dev = local_rank
     if a.share_device and world > 1:
         # before torch's process group and the library create their RCCL communicators
@@ -451,6 +551,7 @@ def main() -> int:
                 "build_options": bopts or None,
                 "layout": ["fused", "split"][info.get("layout", 0)],
                 "hot_cover": round(info.get("hot_cover_ppm", 0) / 1e6, 4),
+                "code_bits": info.get("code_bits"),
                 # --share-device: a correctness rehearsal (ranks share GPUs, RCCL over loopback sockets)
                 "shared_device_rehearsal": bool(a.share_device and world > 1),
             },
@@ -472,6 +573,7 @@ def main() -> int:
                 "spmv_ms_mean": round(spmv_ms, 4),
                 "iter_ms_mean_events": round(st["iter_ms_mean"], 4),
                 "exchange_ms_mean": round(st["exchange_ms_mean"], 4),
+                "gather": gather_roofline(info, spmv_ms) if info.get("layout") == 1 else None,
             },
             "exchange_ms_per_rank": [round(x, 4) for x in xchg_ms] if world > 1 else None,
             "exchange_overlap_ab": overlap,

@@ -95,14 +95,16 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
         o->allgather = v == 1;
         break;
       case PR_BOPT_XCHG_CHUNKS:
-        o->xchg_chunks = v != 0;
+        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_XCHG_CHUNKS: 0 (whole runs) or 1 (overlapped)");
+        o->xchg_chunks = v == 1;
         break;
       case PR_BOPT_HOT_RESERVE:
         if (v < 0 || v > 3) return fail(PR_ERR_INVALID, "PR_BOPT_HOT_RESERVE: 0..3 CUs per XCD");
         o->hot_reserve = (int)v;
         break;
       case PR_BOPT_EPI_WALK:
-        o->epi_walk = v != 0;
+        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_WALK: 0 (class loop) or 1 (per-row walk)");
+        o->epi_walk = v == 1;
         break;
       case PR_BOPT_EPI_NARROW:
         if (v < -1 || v > 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_NARROW: -1 (auto), 0 or 1");
@@ -327,8 +329,9 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
       v[PR_STAT_LAST_L1] = 0.0;
     }
   }
-  PR_TRY(mean_ms(g->spmv_ev, &v[PR_STAT_SPMV_MS_MEAN]));
-  v[PR_STAT_SPMV_LAUNCHES] = (double)g->spmv_ev.size();
+  PR_TRY(mean_ms(g->spmv_ev, &v[PR_STAT_SPMV_MS_MEAN]));  // per interval: scaled to per pass below
+  if (g->spmv_passes > 0) v[PR_STAT_SPMV_MS_MEAN] *= (double)g->spmv_ev.size() / (double)g->spmv_passes;
+  v[PR_STAT_SPMV_LAUNCHES] = (double)g->spmv_passes;
   // an iteration ends when both its kernels (compute stream) and its exchange (xstream, P > 1)
   // are done: per iteration the later of the two ends, measured from the iteration's start
   // (the transfer runs on xstream since round 2)
@@ -462,6 +465,7 @@ int pr_group_reset(pr_graph *const *parts, int32_t n_parts, double teleport, dou
     PR_HIP(hipSetDevice(parts[p]->device));
     PR_TRY(pr::join_exchange(parts[p]));
     PR_HIP(hipStreamSynchronize(parts[p]->stream));
+    parts[p]->xchg_ev.clear();  // the reset's exchange is not an iteration's
   }
   return PR_OK;
 }
@@ -471,12 +475,21 @@ int pr_group_step(pr_graph *const *parts, int32_t n_parts, int32_t iterations) {
   if (iterations < 0) return fail(PR_ERR_INVALID, "iterations < 0");
   for (int32_t p = 0; p < n_parts; ++p)
     if (!parts[p]->grouped || !parts[p]->ready) return fail(PR_ERR_STATE, "pr_group_step before pr_group_reset");
+  std::vector<int> i0((size_t)n_parts, -1);
   for (int32_t it = 0; it < iterations; ++it) {
     for (int32_t p = 0; p < n_parts; ++p) {
       PR_HIP(hipSetDevice(parts[p]->device));
+      if (parts[p]->timing) PR_TRY(pr::time_mark(parts[p], parts[p]->stream, &i0[p]));
       PR_TRY(pr::iter_compute(parts[p]));
     }
     PR_TRY(pr::group_exchange(parts, n_parts, parts[0]->cur));
+    for (int32_t p = 0; p < n_parts; ++p) {  // per part: its kernels and its pack (the copies: xchg_ev)
+      if (!parts[p]->timing) continue;
+      PR_HIP(hipSetDevice(parts[p]->device));
+      int i1 = -1;
+      PR_TRY(pr::time_mark(parts[p], parts[p]->stream, &i1));
+      parts[p]->iter_ev.push_back({i0[p], i1});
+    }
   }
   return PR_OK;
 }

@@ -300,7 +300,7 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   PR_TRY(g->x_sbuf.alloc(sizeof(double) * 2 * (size_t)(send_stride(g) > 0 ? send_stride(g) : 1)));
   PR_HIP(hipStreamSynchronize(s));
   // chunk bounds of the overlapped exchange: one chunk per hot phase (whether the chunks travel
-  // separately: x_chunked, PR_XCHG_CHUNKS / pr_set_option)
+  // separately: x_chunked, PR_BOPT_XCHG_CHUNKS / pr_set_option(PR_OPT_XCHG_CHUNKS))
   g->n_xc = g->C > 1 ? std::max(1, g->C / kXcds) : 1;
   set_exchange_chunking(g);
   PR_TRY(chunk_bounds(g, g->x_send.as<uint32_t>(), g->x_soff, true, &g->x_sch));
@@ -409,16 +409,27 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
     pr_graph *g = parts[q];
     PR_HIP(hipSetDevice(g->device));
     if (whole) {  // whole slices on the compute stream (the A/B reference)
+      int ta = -1, tb = -1;
       for (int p = 0; p < n; ++p) {
         if (p == q) continue;
         PR_HIP(hipStreamWaitEvent(g->stream, parts[p]->xev, 0));
+      }
+      if (g->timing) PR_TRY(time_mark(g, g->stream, &ta));
+      for (int p = 0; p < n; ++p) {
+        if (p == q) continue;
         const int64_t off = (int64_t)p * g->S_pad;
         PR_HIP(hipMemcpyAsync(g->cbuf[buf].as<double>() + off, parts[p]->cbuf[buf].as<double>() + off,
                               sizeof(double) * g->S_pad, hipMemcpyDeviceToDevice, g->stream));
       }
+      if (g->timing) {
+        PR_TRY(time_mark(g, g->stream, &tb));
+        g->xchg_ev.push_back({ta, tb});
+      }
       continue;
     }
     for (int p = 0; p < n; ++p) PR_HIP(hipStreamWaitEvent(g->xstream, parts[p]->x_pack_ev, 0));
+    int ta = -1, tb = -1;  // every pack done -> the last copy into this part
+    if (g->timing) PR_TRY(time_mark(g, g->xstream, &ta));
     const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
     // copy engines (PR_BOPT_XCHG_SDMA): no CU is taken from the receiver's k_spmv_hot phases
     const hipMemcpyKind kind = g->opts.xchg_sdma ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
@@ -436,6 +447,10 @@ int group_exchange(pr_graph *const *parts, int n, int buf) {
                                 g->xstream));
       }
       PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
+    }
+    if (g->timing) {
+      PR_TRY(time_mark(g, g->xstream, &tb));
+      g->xchg_ev.push_back({ta, tb});
     }
     g->x_pending = true;
   }

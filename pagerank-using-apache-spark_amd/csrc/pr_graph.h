@@ -118,7 +118,10 @@ struct pr_graph {
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;  // indices into ev_pool
+  // indices into ev_pool; spmv_ev holds one interval per pass, or one per hot phase (+ the rest of
+  // the pass) when the overlapped exchange gates the phases: spmv_passes passes in all
+  std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;
+  int64_t spmv_passes = 0;
   size_t ev_next = 0;
 
   // gather space (doubles per cbuf): P slices side by side (P = 1, PR_BOPT_EXCHANGE = 1), or
@@ -186,6 +189,7 @@ int n_hot_phases(const pr_graph *g);
 int set_hot_reserve(pr_graph *g, int per_xcd);
 int iter_step(pr_graph *g, int32_t iterations);
 int iter_compute(pr_graph *g);  // one iteration without the exchange; flips g->cur
+// timing (every part's g->timing): per receiving part one xchg_ev interval, its copies on xstream
 int group_exchange(pr_graph *const *parts, int n, int buf);
 // Exchange lists and the gather-space geometry (gsize, own_off, slots); *cmap receives the
 // global -> compacted position map (-1: not read by this part) when the space is compacted.
@@ -195,4 +199,6 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a = nullptr, hipEvent_t ev_b = 
 double *send_runs(const pr_graph *g, int buf);  // the packed send runs paired with gather buffer buf
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
+hipEvent_t next_event(pr_graph *g);  // the next timing event of g's pool (nullptr: creation failed)
+int time_mark(pr_graph *g, hipStream_t s, int *index);  // records one on s; *index into ev_pool
 }  // namespace pr

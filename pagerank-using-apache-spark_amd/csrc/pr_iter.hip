@@ -131,15 +131,6 @@ __global__ __launch_bounds__(kThreads) void k_reset(int64_t n_rows, const double
   if (threadIdx.x == 0) parts[blockIdx.x] = make_double2(dcp, 0.0);
 }
 
-hipEvent_t next_event(pr_graph *g) {
-  if (g->ev_next >= g->ev_pool.size()) {
-    hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    g->ev_pool.push_back(e);
-  }
-  return g->ev_pool[g->ev_next++];
-}
-
 int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n_parts, int in_buf,
                     int out_buf) {
   double *cout = g->cbuf[out_buf].as<double>() + g->own_off;
@@ -160,6 +151,23 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }
 
 }  // namespace
+
+hipEvent_t next_event(pr_graph *g) {
+  if (g->ev_next >= g->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    g->ev_pool.push_back(e);
+  }
+  return g->ev_pool[g->ev_next++];
+}
+
+int time_mark(pr_graph *g, hipStream_t s, int *index) {
+  hipEvent_t e = next_event(g);
+  if (!e) return fail(PR_ERR_HIP, "hipEventCreate failed");
+  PR_HIP(hipEventRecord(e, s));
+  *index = (int)g->ev_next - 1;
+  return PR_OK;
+}
 
 int prepare_hot_kernel() {
   for (int c : {8, 16, 32, 64, 128})
@@ -290,6 +298,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
   g->ready = true;
   g->ev_next = 0;
   g->spmv_ev.clear();
+  g->spmv_passes = 0;
   g->iter_ev.clear();
   g->xchg_ev.clear();
   return PR_OK;
@@ -299,15 +308,33 @@ int iter_compute(pr_graph *g) {
   hipStream_t s = g->stream;
   const int64_t own = g->own_off;
   const int in = g->cur, out = g->cur ^ 1;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (g->timing) {
-    e0 = next_event(g);
-    e1 = next_event(g);
-    if (!e0 || !e1) return fail(PR_ERR_HIP, "hipEventCreate failed");
-    PR_HIP(hipEventRecord(e0, s));
-  }
+  // timing (spmv_ms_mean): the pass's kernels only.  Every start event is recorded after the
+  // stream's wait for the exchange, so a transfer still in flight is never counted as SpMV time;
+  // the overlapped exchange contributes one interval per hot phase.
+  int open_ev = -1;  // ev_pool index of the running interval's start
+  auto mark_start = [&]() -> int {
+    if (!g->timing) return PR_OK;
+    hipEvent_t e = next_event(g);
+    if (!e) return fail(PR_ERR_HIP, "hipEventCreate failed");
+    PR_HIP(hipEventRecord(e, s));
+    open_ev = (int)g->ev_next - 1;
+    return PR_OK;
+  };
+  auto mark_end = [&]() -> int {
+    if (!g->timing) return PR_OK;
+    hipEvent_t e = next_event(g);
+    if (!e) return fail(PR_ERR_HIP, "hipEventCreate failed");
+    PR_HIP(hipEventRecord(e, s));
+    g->spmv_ev.push_back({open_ev, (int)g->ev_next - 1});
+    open_ev = (int)g->ev_next - 1;  // a following interval may start where this one ended
+    return PR_OK;
+  };
+  const int nph = g->C > 1 ? n_hot_phases(g) : 1;
+  const bool phased_wait = g->C > 1 && g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1;
+  if (!phased_wait) PR_TRY(join_exchange(g));
+  else PR_HIP(hipStreamWaitEvent(s, g->x_ev[0], 0));  // phase 0's chunk
+  PR_TRY(mark_start());
   // light rows (all rows when C == 1): fused single pass
-  if (g->C == 1) PR_TRY(join_exchange(g));
   if (g->n_units > 0)
     hipLaunchKernelGGL((k_spmv_units<kPerThread, true>), dim3((unsigned)g->n_units), dim3(kThreads), 0, s,
                        g->units.as<Unit>(), g->rowptr.as<int64_t>(), g->colp.as<int32_t>(),
@@ -316,17 +343,19 @@ int iter_compute(pr_graph *g) {
                        g->slots, g->S_pad, (double)g->V, g->teleport, g->damping);
   int64_t n_parts = g->n_units;
   if (g->C > 1) {  // split layout: class units, long segments, then the epilogue over all rows
-    const int nph = n_hot_phases(g);
-    if (g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1) {
+    if (phased_wait) {
       // overlapped exchange: hot phase c needs only chunk c of the runs received from every peer
       for (int c = 0; c < nph; ++c) {
-        PR_HIP(hipStreamWaitEvent(s, g->x_ev[c], 0));
+        if (c > 0) {
+          PR_TRY(mark_end());
+          PR_HIP(hipStreamWaitEvent(s, g->x_ev[c], 0));
+          PR_TRY(mark_start());
+        }
         PR_TRY(launch_hot(g, in, c, c + 1));
       }
       g->x_pending = false;
-    } else {
-      PR_TRY(join_exchange(g));
-      if (g->n_hunits > 0) PR_TRY(launch_hot(g, in));
+    } else if (g->n_hunits > 0) {
+      PR_TRY(launch_hot(g, in));
     }
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
@@ -349,11 +378,8 @@ int iter_compute(pr_graph *g) {
     n_parts += g->ep_blocks;
   }
   PR_HIP(hipGetLastError());
-  if (g->timing) {
-    PR_HIP(hipEventRecord(e1, s));
-    const int base = (int)g->ev_next - 2;
-    g->spmv_ev.push_back({base, base + 1});
-  }
+  PR_TRY(mark_end());
+  if (g->timing) ++g->spmv_passes;
   PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), n_parts, in, out));
   g->x_packed = (g->x_fused && g->C > 1) ? out : -1;  // the exchange then skips k_pack
   g->cur = out;

@@ -546,6 +546,12 @@ struct EdgeChunk {
   prh_edges le;          // the chunk's local IDs (src, dst) and JSON-made names (arena)
   std::unique_ptr<Interner> in;
   EdgeChunk() : src(le.src), dst(le.dst) {}
+  // src / dst refer into this object's own le: a copy or a move would leave them pointing at the
+  // source object's vectors, so a chunk never moves
+  EdgeChunk(const EdgeChunk &) = delete;
+  EdgeChunk &operator=(const EdgeChunk &) = delete;
+  EdgeChunk(EdgeChunk &&) = delete;
+  EdgeChunk &operator=(EdgeChunk &&) = delete;
 };
 
 void parse_edge_chunk(const char *data, EdgeChunk &c) {

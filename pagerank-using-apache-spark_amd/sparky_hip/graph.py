@@ -68,8 +68,9 @@ class PageRankGraph:
         without links; or, with device_input=True, integer device addresses (e.g. from
         torch ``tensor.data_ptr()``) plus n_edges.  layout: 'auto' (column classes once the
         contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h).  options: build
-        options of pr_graph_create_ex by name (_lib.BUILD_OPTIONS: classes, hot_slots,
-        exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow, codes)."""
+        options of pr_graph_create_ex by name -- _lib.BUILD_OPTIONS is the full list: classes,
+        hot_slots, exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow, codes,
+        pack_fused, xchg_sdma (include/pagerank_hip.h PR_BOPT_*)."""
         L = _lib.load()
         flags = 0
         if dangling == "none":

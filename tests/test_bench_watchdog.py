@@ -36,3 +36,36 @@ def test_non_zero_rank_prints_no_line():
     assert p.returncode == 3
     assert p.stdout.strip() == ""
     assert "attach" in p.stderr
+
+
+# ---- --gpus N: never a 1-GPU number for an N-GPU request ----------------------
+
+def _env_without_launcher(**extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env.update(extra)
+    return env
+
+
+def test_world_size_mismatch_is_an_error_line():
+    env = _env_without_launcher(RANK="0", WORLD_SIZE="3", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert p.returncode != 0
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["value"] is None and "WORLD_SIZE=3" in d["error"] and d["n_gpus"] == 2
+
+
+def test_plain_gpus_n_launches_n_ranks():
+    """Without WORLD_SIZE, `bench.py --gpus 2` starts two ranks under torch.distributed.run as a child
+    and relays rank 0's line.  Here (no GPU) the ranks find no device and say so: the relayed line is
+    an error line for n_gpus 2 and the status is non-zero -- never a line with n_gpus 1."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       capture_output=True, text=True, timeout=240, env=_env_without_launcher())
+    assert p.returncode != 0, p.stdout
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.lstrip().startswith("{")]
+    assert len(lines) == 1, (p.stdout, p.stderr[-3000:])
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] is None and "GPU" in d["error"], d
+    assert "starting 2 ranks" in p.stderr

@@ -10,7 +10,8 @@ What is exercised is the distributed *protocol* the library implements with RCCL
     is identical on every rank with no extra collective).  Two exchanges (pr_exchange.hip):
     "sparse" - rank p sends rank q only the positions of its slice that q's in-links read,
     ascending, then its two slots (grouped send/recv); positions q never reads stay stale (NaN
-    here, so reading one fails the test) - and "allgather" - whole slices (PR_EXCHANGE=allgather).
+    here, so reading one fails the test) - and "allgather" - whole slices (build option
+    PR_BOPT_EXCHANGE = 1, `exchange_allgather` in the Python binding).
 """
 import os
 

@@ -28,12 +28,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, extra, scale=20, timeout=280):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", str(world), "--share-device", "--scale", str(scale), "--steps", "6", "--warmup", "2",
-           "--parity-iters", "10", "--stage-timeout", "150"] + extra
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
+def _run(world, extra, scale=20, timeout=280, launcher=True, steps=6, warmup=2):
+    """launcher=False: a plain `python bench.py --gpus N`, which starts its N ranks itself."""
+    cmd = [sys.executable]
+    if launcher:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+                f"--master-port={_free_port()}"]
+    cmd += [os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--share-device", "--scale", str(scale), "--steps",
+            str(steps), "--warmup", str(warmup), "--parity-iters", "10", "--stage-timeout", "150"] + extra
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "8"))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=env)
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert p.returncode == 0 and lines, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-5000:]}"
@@ -69,3 +73,29 @@ def test_rccl_exchange_on_shared_device(world, extra):
         assert ab is not None and ab["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1",
                                                    "chunked_reserve2")
         assert par["max_rel_overlapped_exchange"] <= RANK_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(320)
+def test_plain_bench_gpus_2_runs_two_ranks():
+    """`python bench.py --gpus 2` with no launcher around it (the driver's BENCH command shape) runs two
+    ranks -- it starts torch.distributed.run itself -- and reports n_gpus 2 with oracle parity."""
+    line = _run(2, [], launcher=False)
+    assert line["n_gpus"] == 2 and line["value"] is not None
+    assert line["parity"]["ranks_from"] == "2 rank(s)" and line["parity"]["every_row_owned_once"] is True
+    assert line["parity"]["max_rel"] <= RANK_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_rccl_default_policy_at_baseline_size():
+    """BASELINE.json configs[2] (Erdos-Renyi s24) at P = 4 through the RCCL transport with the default
+    build policy -- 64 classes, piece codes, the epilogue's fused pack, per-peer runs -- both exchange
+    modes checked against the oracle after 10 iterations (Sparky.java:187, :192, :229-233)."""
+    line = _run(4, ["--graph", "er", "--serial-build"], scale=24, timeout=560, steps=4, warmup=1)
+    assert line["n_gpus"] == 4 and line["config"]["build_options"] is None
+    assert line["config"]["exchange_doubles_per_iter_rank0"] > 0
+    par = line["parity"]
+    assert par["every_row_owned_once"] is True
+    assert par["max_rel"] <= RANK_TOL and par["max_rel_overlapped_exchange"] <= RANK_TOL
+    assert line["roofline"]["classes"] == 64 and line["config"]["code_bits"] in (20, 24)

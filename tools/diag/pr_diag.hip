@@ -113,6 +113,24 @@ __global__ __launch_bounds__(256) void k_scalar_probe(const double *__restrict__
   }
   if (acc == 12345.0 && (threadIdx.x & 63) == 0) out[w] = acc;
 }
+// LDS probe: one 1024-thread workgroup per CU holds a `slots`-double table in LDS (the size of
+// k_spmv_hot's hot set) and every thread reads `per_thread` random slots, 8 independent reads in
+// flight -- the LDS side of the SpMV's gathers (roofline.gather in bench.py).
+__global__ __launch_bounds__(1024) void k_lds_probe(int slots, int per_thread, uint32_t seed, double *__restrict__ out) {
+  extern __shared__ double tab[];
+  for (int i = threadIdx.x; i < slots; i += 1024) tab[i] = (double)i;
+  __syncthreads();
+  const uint32_t t = blockIdx.x * 1024u + threadIdx.x;
+  double acc = 0.0;
+  for (int j0 = 0; j0 < per_thread; j0 += 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = tab[mix32(t * 8191u + (uint32_t)(j0 + k) + seed) % (uint32_t)slots];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += v[k];
+  }
+  if (acc == 12345.0) out[t] = acc;
+}
 // CU-mask probe: every workgroup (one wave) records its XCC id and raw HW_ID register (CU, SH, SE
 // fields), so a stream's CU-mask bits can be mapped to physical CUs and XCDs.
 __global__ void k_cu_probe(uint32_t *__restrict__ out) {
@@ -260,6 +278,35 @@ int prd_stream_probe(int device, int64_t table_bytes, int64_t n_loads, int width
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
   (void)hipFree(tab);
+  (void)hipFree(out);
+  return 0;
+}
+
+// LDS probe (see k_lds_probe): blocks x 1024 threads x per_thread random 8-byte LDS reads; ms per launch.
+int prd_lds_probe(int device, int blocks, int slots, int per_thread, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  const size_t lds = sizeof(double) * (size_t)slots;
+  PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_lds_probe), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds));
+  void *out = nullptr;
+  PR_HIP(hipMalloc(&out, sizeof(double) * 1024 * (size_t)blocks));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i)
+      hipLaunchKernelGGL(k_lds_probe, dim3(blocks), dim3(1024), lds, 0, slots, per_thread, 977u * (uint32_t)i,
+                         (double *)out);
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
   (void)hipFree(out);
   return 0;
 }

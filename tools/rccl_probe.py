@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=18)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--exchange", choices=["sparse", "allgather"], default="sparse",
+                    help="per-peer runs (the default) or whole-slice all-gather (build option exchange_allgather)")
     a = ap.parse_args()
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
@@ -39,7 +41,8 @@ def main():
     sparky_hip.gen_rmat(0, a.scale, E, s.data_ptr(), d.data_ptr(), seed=7)
     V = sparky_hip.intern_device(0, E, 1 << a.scale, s.data_ptr(), d.data_ptr())
     g = sparky_hip.PageRankGraph(V, s.data_ptr(), d.data_ptr(), device_input=True, n_edges=E, part=rank,
-                                 n_parts=world, keep_canonical=False)
+                                 n_parts=world, keep_canonical=False,
+                                 options={"exchange_allgather": 1} if a.exchange == "allgather" else None)
     obj = [sparky_hip.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     try:
@@ -65,7 +68,7 @@ def main():
                                       keep_canonical=False) as g1:
             r1, _ = g1.run(a.iters)
         rel = float(np.max(np.abs(merged - r1) / np.abs(r1)))
-        print(f"RCCL {world} ranks on one GPU ({os.environ.get('PR_EXCHANGE', 'sparse')}): max rel vs 1 part {rel:.3e}",
+        print(f"RCCL {world} ranks on one GPU ({a.exchange}): max rel vs 1 part {rel:.3e}",
               flush=True)
         assert rel <= 1e-12
     dist.destroy_process_group()
