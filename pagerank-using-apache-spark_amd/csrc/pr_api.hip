@@ -43,7 +43,7 @@ void DevBuf::reset() {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + partial2.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes + cside.bytes;
   return b;
@@ -117,6 +117,10 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
       case PR_BOPT_PACK_FUSED:
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_PACK_FUSED: 0 (pack kernel) or 1 (in the epilogue)");
         o->pack_fused = v == 1;
+        break;
+      case PR_BOPT_EPI_OVERLAP:
+        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_OVERLAP: 0 (after the pass) or 1 (beside the next hot phases)");
+        o->epi_overlap = v == 1;
         break;
       case PR_BOPT_XCHG_SDMA:
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_XCHG_SDMA: 0 (device copies) or 1 (copy engines)");
@@ -221,7 +225,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->C == 1 ? 0 : 3, g->gather_est, g->n_walk_groups, g->layout,
+                                    g->C == 1 ? 0 : (g->epi_overlap ? 4 : 3), g->gather_est, g->n_walk_groups, g->layout,
                                     g->hot_cover_ppm, g->C > 1 ? (g->code == pr::kCodeC20 || g->code == pr::kCodeC20P ? 20 : g->code == pr::kCodeC24 || g->code == pr::kCodeC24P ? 24 : 32) : 0};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
@@ -271,6 +275,7 @@ int pr_get_ranks(pr_graph *g, double *ranks_out) {
   if (!g || !ranks_out) return fail(PR_ERR_INVALID, "NULL argument");
   if (!g->ready) return fail(PR_ERR_STATE, "pr_get_ranks before pr_reset");
   DeviceGuard dg(g->device);
+  PR_TRY(pr::join_exchange(g));  // an overlapped epilogue may still be writing r
   std::vector<double> loc((size_t)g->n_rows);
   if (g->n_rows > 0)
     PR_HIP(hipMemcpyAsync(loc.data(), g->r.p, sizeof(double) * g->n_rows, hipMemcpyDeviceToHost, g->stream));
@@ -283,6 +288,7 @@ int pr_get_ranks(pr_graph *g, double *ranks_out) {
 int pr_set_timing(pr_graph *g, int32_t enable) {
   if (!g) return fail(PR_ERR_INVALID, "NULL graph");
   g->timing = enable != 0;
+  if (!g->timing) g->overlap_start_ev = -1;
   return PR_OK;
 }
 
@@ -509,12 +515,17 @@ void pr_graph_destroy(pr_graph *g) {
   DeviceGuard dg(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->xstream) (void)hipStreamSynchronize(g->xstream);
+  if (g->estream) (void)hipStreamSynchronize(g->estream);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
   if (g->xev) (void)hipEventDestroy(g->xev);
   for (hipEvent_t e : g->x_ev) (void)hipEventDestroy(e);
   if (g->x_pack_ev) (void)hipEventDestroy(g->x_pack_ev);
   if (g->xstream) (void)hipStreamDestroy(g->xstream);
+  for (hipEvent_t e : g->e_chunk) (void)hipEventDestroy(e);
+  if (g->e_hot) (void)hipEventDestroy(g->e_hot);
+  if (g->e_fin) (void)hipEventDestroy(g->e_fin);
+  if (g->estream) (void)hipStreamDestroy(g->estream);
   g->ev_pool.clear();
   hipStream_t s = g->stream;
   g->stream = nullptr;

@@ -481,15 +481,10 @@ __global__ __launch_bounds__(64) void k_fill_piece(int64_t n_units, const Unit *
           const int32_t v = col[s0 + i];
           const int32_t pos = v & 0x7FFFFFFF;
           const int32_t h = hotidx[pos];
-          if (h) {
-            idx = (uint32_t)h;
-            ++nhot;
-          } else {
-            int p = 0;
-            while (p < P && !(pos >= px[3 * p] && pos < px[3 * p + 1])) ++p;
-            if (p == P) ++nb;
-            else idx = (uint32_t)(nh + 1 + px[3 * p + 2] + (pos - px[3 * p]));
-          }
+          bool miss = false;
+          idx = piece_encode(pos, h, px, P, nh, &miss);  // pr_pieces.h
+          nhot += h ? 1 : 0;
+          nb += miss ? 1 : 0;
           if (u.meta >= 0 && v < 0) side |= (SideT)1 << j;  // segment end (STREAM units)
         }
         lo[j] = idx & 0xFFFFu;
@@ -526,29 +521,7 @@ static int plan_pieces(const pr_graph *g, const int32_t *cmap, int C, int P, Pie
   std::vector<int32_t> h((size_t)(2 * np));
   PR_HIP(hipMemcpyAsync(h.data(), lohi.p, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s));
   PR_HIP(hipStreamSynchronize(s));
-  pp->pc.assign((size_t)(3 * np), 0);
-  pp->tbl.assign((size_t)C * kPieceTblWords, 0);
-  pp->vmax = 0;
-  for (int x = 0; x < C; ++x) {
-    int64_t v = 0;
-    for (int p = 0; p < P; ++p) {
-      const int64_t i = (int64_t)x * P + p;
-      const int32_t g0 = h[(size_t)i], g1 = h[(size_t)(np + i)];
-      int32_t *e = &pp->pc[(size_t)(3 * i)];
-      if (g1 <= g0) {  // empty piece: matches nothing
-        e[0] = e[1] = e[2] = 0;
-        continue;
-      }
-      v = (v + kPieceAlign - 1) / kPieceAlign * kPieceAlign;
-      e[0] = g0;
-      e[1] = g1;
-      e[2] = (int32_t)std::min<int64_t>(v, INT32_MAX);
-      for (int64_t t = v >> kPieceShift; t <= (v + (g1 - g0) - 1) >> kPieceShift && t < kPieceTbl; ++t)
-        pp->tbl[(size_t)(x * kPieceTblWords + t)] = (int32_t)(uint32_t)(8u * (uint32_t)(g0 - (int32_t)v));
-      v += g1 - g0;
-    }
-    pp->vmax = std::max(pp->vmax, v);
-  }
+  pp->vmax = piece_tables(h.data(), C, P, &pp->pc, &pp->tbl);  // pr_pieces.h
   return PR_OK;
 }
 
@@ -844,6 +817,17 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                                                      : kCodeU32;
       if (code_is_piece(g->code)) slots = ps;
     }
+    // epilogue overlap: the hot set leaves LDS room for two one-wave epilogue workgroups per CU
+    // (their 8 KiB windows, rounded up to 1 KiB allocation blocks)
+    const bool overlap = g->opts.epi_overlap && P == 1 && C >= 2 * kXcds && C <= kWave;
+    if (overlap) {
+      HotGeom t{};
+      t.P = 1;
+      const size_t epi = 2 * ((epi_grp_lds(true) + 1023) & ~size_t(1023));
+      for (t.Kp = slots; t.Kp > 0 && t.lds_bytes() + epi > (size_t)kHotLdsBytes; --t.Kp) {
+      }
+      slots = t.Kp;
+    }
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
@@ -895,6 +879,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     }
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
+    if (overlap) {  // the hot kernel of iteration i + 1 fills the other buffer
+      PR_TRY(g->partial2.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
+      g->epi_overlap = true;
+    }
     g->n_slots = poff[C];
     PR_HIP(hipMemcpyAsync(g->hucum.p, sp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
@@ -989,8 +977,27 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->epi_narrow = epi_narrow_ok(C) && (g->opts.epi_narrow < 0 ? auto_narrow : g->opts.epi_narrow != 0);
     g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
   }
+  int64_t ep_parts = g->ep_blocks;
+  if (g->epi_overlap) {
+    // chunk c = the rows of class regions [8c, 8c + 8): Q_pad / 64 groups of 8 blocks (Q_pad is a
+    // multiple of 64, so chunks start on group boundaries)
+    g->n_echunks = n_hot_phases(g);
+    g->ep_chunk_groups = g->Q_pad / kWave;
+    if (g->ep_chunk_groups * g->n_echunks != (g->nblk + kEpiGroup - 1) / kEpiGroup)
+      return fail(PR_ERR_STATE, "epilogue chunks do not tile the groups");
+    int n_cu = 0;
+    PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
+    g->ep_blocks0 = (int)grid_for(g->ep_chunk_groups, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
+    g->ep_thin = 2 * n_cu;
+    ep_parts = std::max<int64_t>(ep_parts, g->ep_blocks0 + (int64_t)(g->n_echunks - 1) * g->ep_thin);
+    PR_HIP(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
+    g->e_chunk.assign(g->n_echunks, nullptr);
+    for (auto &e : g->e_chunk) PR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    PR_HIP(hipEventCreateWithFlags(&g->e_hot, hipEventDisableTiming));
+    PR_HIP(hipEventCreateWithFlags(&g->e_fin, hipEventDisableTiming));
+  }
   // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
-  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + g->ep_blocks + 1)));
+  PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + ep_parts + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 
   if (g->flags & PR_NO_CANONICAL) {

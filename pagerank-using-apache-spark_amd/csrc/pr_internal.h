@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "pagerank_hip.h"
+#include "pr_pieces.h"
 
 namespace pr {
 
@@ -116,6 +117,11 @@ constexpr int kEpiThreads = 256;  // 4 waves, 32.1 KiB of LDS: four workgroups p
 constexpr int kEpiThreadsNarrow = 64;  // one wave64
 inline bool epi_narrow_ok(int C) { return C <= 64; }  // one-wave workgroups: at most 64 classes
 inline int epi_grp_threads(bool narrow) { return narrow ? kEpiThreadsNarrow : kEpiThreads; }
+// dynamic LDS of k_epilogue_grp: per wave its window of kEpiWin slots + the zero slot and padding,
+// then per wave a double2 for the block sum
+inline size_t epi_grp_lds(bool narrow) {
+  return sizeof(double) * (size_t)(epi_grp_threads(narrow) / 64) * (kEpiWin + 4);
+}
 
 // per-row info word: out-degree | flags
 constexpr uint32_t kRowDegMask = (1u << 28) - 1;
@@ -164,13 +170,7 @@ constexpr int kCodeC20 = 1;
 constexpr int kCodeC24 = 2;
 constexpr int kCodeC20P = 3;
 constexpr int kCodeC24P = 4;
-constexpr int kC20IdxBits = 19;
-constexpr int kC24IdxBits = 20;
-constexpr int kPieceShift = 12;
-constexpr int kPieceAlign = 1 << kPieceShift;
-constexpr int kPieceTbl = (1 << kC24IdxBits) >> kPieceShift;  // 256 blocks cover any 20-bit index
-constexpr int kPieceTblWords = kPieceTbl + 2;                 // + the sentinel, rounded to 8 bytes
-constexpr int kPieceTblSlots = kPieceTblWords / 2;            // in doubles
+// kC20IdxBits, kC24IdxBits and the piece-table constants: pr_pieces.h
 constexpr __host__ __device__ bool code_is_piece(int code) { return code >= kCodeC20P; }
 // LDS of k_spmv_hot: the hot set (slot 0 = 0.0, then the hot contributions of every part), one
 // more 0.0 slot (where compact cold entries point their LDS read), the workgroup's unit counter,

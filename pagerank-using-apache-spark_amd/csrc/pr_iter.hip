@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(int64_t n_rows, const double
 }
 
 int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n_parts, int in_buf,
-                    int out_buf) {
+                    int out_buf, hipStream_t stream) {
   double *cout = g->cbuf[out_buf].as<double>() + g->own_off;
   PackSlots ps{};
   if (g->x_fused) {  // the slots of every peer's run (its last two entries)
@@ -140,7 +140,7 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
     for (int q = 0; q < g->nparts; ++q)
       if (q != g->part) ps.off[ps.n++] = g->x_soff[q + 1] - 2;
   }
-  hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, g->stream, n_long,
+  hipLaunchKernelGGL(k_finalize, dim3(g->fin_blocks), dim3(kThreads), 0, stream, n_long,
                      g->lr_row.as<int32_t>(), g->lr_p0.as<int32_t>(), g->piece_part.as<double>(),
                      parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[in_buf].as<double>(), cout, g->slots, (double)g->V,
@@ -151,6 +151,8 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
 }
 
 }  // namespace
+
+double *partial_buf(const pr_graph *g) { return (g->pbuf ? g->partial2 : g->partial).as<double>(); }
 
 hipEvent_t next_event(pr_graph *g) {
   if (g->ev_next >= g->ev_pool.size()) {
@@ -254,7 +256,7 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
                                      : k_spmv_hot<kCodeU32>;
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
-                     (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),
+                     (uint32_t)(sizeof(double) * g->gsize), partial_buf(g), g->poff.as<int64_t>(),
                      g->piece_part.as<double>(), g->hpos.as<int32_t>(), g->ptab.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
@@ -263,6 +265,10 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
 void set_exchange_chunking(pr_graph *g) { g->x_chunked = g->opts.xchg_chunks && g->n_xc > 1; }
 
 int join_exchange(pr_graph *g) {
+  if (g->epi_pending) {  // the overlapped epilogue (and its finalize) still on estream
+    PR_HIP(hipStreamWaitEvent(g->stream, g->e_fin, 0));
+    g->epi_pending = false;
+  }
   if (!g->x_pending) return PR_OK;
   PR_HIP(hipStreamWaitEvent(g->stream, g->x_ev.back(), 0));  // chunks are recorded in order
   g->x_pending = false;
@@ -282,13 +288,15 @@ int iter_reset(pr_graph *g, const double *init_host) {
     PR_HIP(hipStreamSynchronize(s));
   }
   g->cur = 0;
+  g->pbuf = 0;
+  g->overlap_start_ev = -1;
   g->x_packed = -1;
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
                      dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[0].as<double>() + own, g->reset_part.as<double2>());
   PR_HIP(hipGetLastError());
-  PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0));
+  PR_TRY(launch_finalize(g, 0, g->reset_part.as<double2>(), g->reset_blocks, 0, 0, s));
   if (!g->grouped) {
     PR_TRY(exchange(g, 0));
     PR_TRY(join_exchange(g));
@@ -304,7 +312,69 @@ int iter_reset(pr_graph *g, const double *init_host) {
   return PR_OK;
 }
 
+// The epilogue overlapped with the next iteration's hot phases (PR_BOPT_EPI_OVERLAP; P = 1, split
+// layout).  Compute stream: hot phase c of this iteration waits for chunk c of the previous
+// epilogue (the contributions of the class regions it reads), then k_seg_reduce.  estream: the
+// epilogue of this iteration in chunks, chunk c recorded as e_chunk[c], then k_finalize.  The hot
+// kernel writes the partial buffer the running epilogue does not read (pbuf flips per iteration);
+// everything an epilogue reads or writes besides -- r, c' of its chunk's rows, the dc slots -- no
+// hot phase touches, and estream runs the epilogues and finalizes in iteration order.  Timing: one
+// interval per pass, from the previous pass's finalize (the first: this pass's phase 0) to this
+// finalize, so the intervals tile the timed run.
+int iter_compute_overlap(pr_graph *g) {
+  hipStream_t s = g->stream, es = g->estream;
+  const int in = g->cur, out = g->cur ^ 1;
+  const int nph = n_hot_phases(g);
+  double *part = partial_buf(g);
+  for (int c = 0; c < nph; ++c) {
+    if (g->epi_pending) PR_HIP(hipStreamWaitEvent(s, g->e_chunk[c], 0));
+    if (c == 0 && g->timing && g->overlap_start_ev < 0) PR_TRY(time_mark(g, s, &g->overlap_start_ev));
+    if (g->n_hunits > 0) PR_TRY(launch_hot(g, in, c, c + 1));
+  }
+  if (g->n_segs > 0)
+    hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
+                       g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(), part);
+  PR_HIP(hipEventRecord(g->e_hot, s));
+  PR_HIP(hipStreamWaitEvent(es, g->e_hot, 0));
+  const int64_t own = g->own_off;
+  double2 *ep_part = g->unit_part.as<double2>() + g->n_units;
+  int64_t n_parts = 0;
+  for (int c = 0; c < g->n_echunks; ++c) {
+    const bool fat = c == 0;  // alone on the critical path: the full grid
+    const bool narrow = fat ? g->epi_narrow : true;
+    const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, narrow);
+    const int blocks = fat ? g->ep_blocks0 : g->ep_thin;
+    const int64_t g0 = (int64_t)c * g->ep_chunk_groups;
+    hipLaunchKernelGGL(epi, dim3(blocks), dim3(epi_grp_threads(narrow)), epi_grp_lds(narrow), es, g->nblk, g0,
+                       g0 + g->ep_chunk_groups, part, g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                       g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
+                       (double)g->V, g->teleport, g->damping, ep_part + n_parts, g->eoff.as<int64_t>(),
+                       g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(), PackDst{});
+    n_parts += blocks;
+    PR_HIP(hipEventRecord(g->e_chunk[c], es));
+  }
+  PR_HIP(hipGetLastError());
+  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + n_parts, in, out, es));
+  PR_HIP(hipEventRecord(g->e_fin, es));
+  if (g->timing) {
+    int e = -1;
+    PR_TRY(time_mark(g, es, &e));
+    g->spmv_ev.push_back({g->overlap_start_ev, e});
+    g->iter_ev.push_back({g->overlap_start_ev, e});
+    ++g->spmv_passes;
+    g->overlap_start_ev = e;
+  } else {
+    g->overlap_start_ev = -1;
+  }
+  g->epi_pending = true;
+  g->pbuf ^= 1;
+  g->cur = out;
+  ++g->iters_done;
+  return PR_OK;
+}
+
 int iter_compute(pr_graph *g) {
+  if (g->epi_overlap) return iter_compute_overlap(g);
   hipStream_t s = g->stream;
   const int64_t own = g->own_off;
   const int in = g->cur, out = g->cur ^ 1;
@@ -360,7 +430,7 @@ int iter_compute(pr_graph *g) {
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
-                         g->partial.as<double>());
+                         partial_buf(g));
     const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
     PackDst pd{};  // fused pack: c' straight into the send runs paired with buffer `out`
     if (g->x_fused) {
@@ -370,7 +440,7 @@ int iter_compute(pr_graph *g) {
       for (int q = 0; q < g->nparts; ++q) pd.soff[q] = g->x_soff[q];
     }
     hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
-                       g->nblk, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                       g->nblk, (int64_t)0, (g->nblk + kEpiGroup - 1) / kEpiGroup, partial_buf(g), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                        g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                        (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
                        g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
@@ -380,7 +450,7 @@ int iter_compute(pr_graph *g) {
   PR_HIP(hipGetLastError());
   PR_TRY(mark_end());
   if (g->timing) ++g->spmv_passes;
-  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), n_parts, in, out));
+  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), n_parts, in, out, s));
   g->x_packed = (g->x_fused && g->C > 1) ? out : -1;  // the exchange then skips k_pack
   g->cur = out;
   ++g->iters_done;
@@ -390,6 +460,10 @@ int iter_compute(pr_graph *g) {
 int iter_step(pr_graph *g, int32_t iterations) {
   if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
   if (g->grouped) return fail(PR_ERR_STATE, "graph belongs to a group: use pr_group_step");
+  if (g->epi_overlap) {  // P = 1: no exchange; the pass records its own intervals
+    for (int32_t it = 0; it < iterations; ++it) PR_TRY(iter_compute(g));
+    return PR_OK;
+  }
   for (int32_t it = 0; it < iterations; ++it) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g->timing) {

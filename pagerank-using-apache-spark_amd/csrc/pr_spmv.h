@@ -410,9 +410,8 @@ struct ClassSrc {
 // read the 0 sentinel and stay out of range).
 template <bool PIECE>
 __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs) {
-  uint32_t go = b8 - cs.hb;
-  if constexpr (PIECE) go += cs.tbl[min(go >> (kPieceShift + 3), (uint32_t)kPieceTbl)];
-  return go;
+  if constexpr (PIECE) return piece_cold_offset(b8, cs.hb, cs.tbl);  // pr_pieces.h
+  else return b8 - cs.hb;
 }
 
 // The unit's values: per entry an LDS read (hot) and a range-checked gather-space load (cold),
@@ -787,9 +786,11 @@ __device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
 // class order -- as many steps per block as its busiest row has classes, instead of one per class
 // -- and the sums are bitwise those of the class loop (whose absent classes add an exact +0).
 // (at least 4 waves per SIMD: the LDS of four four-wave workgroups per CU)
+//
+// Groups [g_lo, g_hi) only: the whole pass, or one chunk of the overlapped epilogue (PR_BOPT_EPI_OVERLAP).
 template <int C, bool WALK, int NT>
 __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
-    int64_t nblk, const double *__restrict__ partial, const void *__restrict__ rmask_v,
+    int64_t nblk, int64_t g_lo, int64_t g_hi, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part, const int64_t *__restrict__ eoff,
@@ -808,9 +809,8 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
   if (lane == 0) win[W] = 0.0;  // the zero slot (never a DMA target: fill <= W)
   const double tdc = dc_from_slots(cin, sp) / n_vertices;
   double dcp = 0.0, l1p = 0.0;
-  const int64_t ngrp = (nblk + G - 1) / G;
   const int64_t nw = (int64_t)gridDim.x * NW;
-  for (int64_t gi = (int64_t)blockIdx.x * NW + wv; gi < ngrp; gi += nw) {
+  for (int64_t gi = g_lo + (int64_t)blockIdx.x * NW + wv; gi < g_hi; gi += nw) {
     const int64_t b0 = gi * G;
     const int nb = (int)min((int64_t)G, nblk - b0);
     uint32_t mw[MW][G], info[G];
@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, con
 
 // k_epilogue_grp instantiations: walk (<= 64 classes), one-wave (narrow, <= 64 classes) or
 // four-wave workgroups
-using EpiGrpFn = void (*)(int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
+using EpiGrpFn = void (*)(int64_t, int64_t, int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
                           double *, const double *, SlotPos, double, double, double, double2 *, const int64_t *,
                           const uint16_t *, const uint8_t *, const int32_t *, PackDst);
 template <int C>
@@ -1079,9 +1079,6 @@ inline EpiGrpFn epi_grp_kernel(int C, bool walk, bool narrow) {
     case 64: return epi_grp_kernel_c<64>(walk, narrow);
     default: return epi_grp_kernel_c<128>(false, false);
   }
-}
-inline size_t epi_grp_lds(bool narrow) {
-  return sizeof(double) * (size_t)(epi_grp_threads(narrow) / kWave) * (kEpiWin + 4);
 }
 
 }  // namespace pr

@@ -715,3 +715,46 @@ def test_compact_codes_widen_then_fall_back(hip, oracle_c, V, bits):
             assert g.info()["code_bits"] == 32
             r32, _ = g.run(4)
         assert np.array_equal(r32, ranks)
+
+@pytest.mark.parametrize("classes,walk", [(16, 1), (32, 1), (64, 1), (64, 0)])
+def test_epilogue_overlap_bitwise(hip, oracle_c, classes, walk):
+    """PR_BOPT_EPI_OVERLAP: the epilogue of iteration i runs in class-region chunks on a second stream
+    beside the hot phases of i + 1, on double-buffered partial slots, with a hot set trimmed to leave
+    LDS for two epilogue waves per CU.  Whether a value comes from LDS or the gather space and which
+    stream runs a chunk do not change any sum: the ranks, dc and L1 of every iteration are bitwise
+    those of the serial pass, through the step API (no host sync between iterations), through pr_run
+    with a per-iteration callback (a join every iteration) and after a reset mid-stream."""
+    rng = np.random.default_rng(classes + walk)
+    V = 60000
+    src, dst = random_edges(rng, V, 900000, hub_frac=0.02)
+    iters = 9
+    ref = oracle_c.run(oracle_c.build_csr(V, src, dst), iters, keep_history=True)
+    out = {}
+    for ov in (0, 1):
+        opts = {"classes": classes, "epi_walk": walk, "epi_overlap": ov}
+        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split", options=opts) as g:
+            info = g.info()
+            assert info["classes"] == classes and info["epilogue"] == (4 if ov else 3)
+            if ov:
+                assert info["hot_slots"] < 18429  # LDS left for the co-resident epilogue waves
+            hist = []
+            ranks_cb, st = g.run(iters, want_ranks_in_callback=True, callback=lambda it, r, s: hist.append((r, s)))
+            g.reset()
+            g.step(3)  # a reset with the overlapped epilogue still in flight must join it
+            g.reset()
+            g.set_timing(True)
+            g.step(iters)
+            g.sync()
+            stats = g.stats()
+            g.set_timing(False)
+            out[ov] = (ranks_cb, hist, g.ranks(), stats)
+    r0, h0, s0, st0 = out[0]
+    r1, h1, s1, st1 = out[1]
+    assert np.array_equal(r0, r1) and np.array_equal(s0, s1) and np.array_equal(r1, s1)
+    for (a, sa), (b, sb) in zip(h0, h1):
+        assert np.array_equal(a, b)
+        assert sa.dc == sb.dc and sa.l1 == sb.l1
+    assert st1["spmv_launches"] == iters and st1["spmv_ms_mean"] > 0 and st1["iter_ms_mean"] > 0
+    assert st0["last_dc"] == st1["last_dc"] and st0["last_l1"] == st1["last_l1"]
+    for it in range(iters):
+        assert max_rel(h1[it][0], ref["history"][it]) <= RANK_TOL

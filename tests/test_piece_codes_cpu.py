@@ -4,61 +4,75 @@ The build (pr_build.hip plan_pieces / k_fill_piece) lays every class's pieces --
 one sub-run of each peer's received run -- out in part order at kPieceAlign-aligned starts of a
 virtual index space and writes, per class, a table of byte deltas per 4096-entry block plus a 0
 sentinel; k_spmv_hot (pr_spmv.h cold_offset) turns an entry's index back into a byte offset with
-u32 arithmetic: go = 8*idx - 8*(nh+1); go += tbl[min(go >> 15, 256)].  This restates both sides in
-numpy and checks, for random piece layouts, that every cold source decodes to its own gather
-position and that hot and padding entries decode to offsets >= 2^31 (out of range of any gather
-space, so the range-checked load returns 0 and costs no memory request).  Host logic only: the
+u32 arithmetic: go = 8*idx - 8*(nh+1); go += tbl[min(go >> 15, 256)].  All three live in
+csrc/pr_pieces.h, which the library and this test's shim (host/pieces_shim.cpp) compile alike, so
+the test runs the product's own code: for random piece layouts every cold source
+decodes to its own gather position, and hot and padding entries decode to offsets >= 2^31 (out of
+range of any gather space, so the range-checked load returns 0 and costs no memory request).  The
 GPU tests (tests/test_gpu_parity.py::test_piece_codes_bitwise) run the kernels themselves.
 """
+import ctypes
+import os
+
 import numpy as np
 import pytest
 
-PIECE_SHIFT = 12
-PIECE_ALIGN = 1 << PIECE_SHIFT
-PIECE_TBL = (1 << 20) >> PIECE_SHIFT  # 256
-TBL_WORDS = PIECE_TBL + 2
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHIM = os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpr_pieces_shim.so")
+PIECE_TBL = 256
 
 
-def plan_pieces(lo, hi):
-    """lo/hi[x, p] -> pc[x, p] = (g0, g1, v0), tbl[x, TBL_WORDS] (u32 byte deltas), vmax."""
+@pytest.fixture(scope="module")
+def shim():
+    if not os.path.exists(SHIM):
+        import subprocess
+
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host")], check=True)
+    lib = ctypes.CDLL(SHIM)
+    P_ = ctypes.c_void_p
+    lib.prp_tbl_words.restype = ctypes.c_int
+    lib.prp_tables.argtypes = [P_, ctypes.c_int, ctypes.c_int, P_, P_]
+    lib.prp_tables.restype = ctypes.c_int64
+    lib.prp_encode.argtypes = [P_, P_, ctypes.c_int64, P_, ctypes.c_int, ctypes.c_int, P_, P_]
+    lib.prp_cold_offset.argtypes = [P_, ctypes.c_int64, ctypes.c_int, P_, P_]
+    return lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def plan_pieces(shim, lo, hi):
+    """lo/hi[x, p] -> pc[x, p] = (g0, g1, v0), tbl[x, words] (u32 byte deltas), vmax -- the build's plan."""
     C, P = lo.shape
-    pc = np.zeros((C, P, 3), np.int64)
-    tbl = np.zeros((C, TBL_WORDS), np.uint32)
-    vmax = 0
-    for x in range(C):
-        v = 0
-        for p in range(P):
-            g0, g1 = int(lo[x, p]), int(hi[x, p])
-            if g1 <= g0:
-                continue
-            v = (v + PIECE_ALIGN - 1) // PIECE_ALIGN * PIECE_ALIGN
-            pc[x, p] = (g0, g1, v)
-            for t in range(v >> PIECE_SHIFT, min(((v + g1 - g0 - 1) >> PIECE_SHIFT) + 1, PIECE_TBL)):
-                tbl[x, t] = np.uint32((8 * (g0 - v)) & 0xFFFFFFFF)
-            v += g1 - g0
-        vmax = max(vmax, v)
-    return pc, tbl, vmax
+    lohi = np.concatenate([lo.reshape(-1), hi.reshape(-1)]).astype(np.int32)
+    pc = np.zeros(3 * C * P, np.int32)
+    W = shim.prp_tbl_words()
+    tbl = np.zeros(C * W, np.int32)
+    vmax = shim.prp_tables(_p(lohi), C, P, _p(pc), _p(tbl))
+    return pc.reshape(C, P, 3).astype(np.int64), tbl.view(np.uint32).reshape(C, W), int(vmax)
 
 
-def encode(pos, hot_slot, x, pc, nh):
+def encode(shim, pos, hot_slot, x, pc, nh):
     """k_fill_piece: the hot slot, or nh + 1 + the virtual index; -1 when no piece holds pos."""
-    if hot_slot:
-        return hot_slot
-    for g0, g1, v0 in pc[x]:
-        if g0 <= pos < g1:
-            return nh + 1 + v0 + (pos - g0)
-    return -1
+    P = pc.shape[1]
+    px = np.ascontiguousarray(pc[x].reshape(-1), np.int32)
+    a_pos, a_hot = np.array([pos], np.int32), np.array([hot_slot], np.int32)
+    idx, bad = np.zeros(1, np.uint32), np.zeros(1, np.uint8)
+    shim.prp_encode(_p(a_pos), _p(a_hot), 1, _p(px), P, nh, _p(idx), _p(bad))
+    return -1 if bad[0] else int(idx[0])
 
 
-def cold_offset(idx, x, tbl, nh):
-    """pr_spmv.h cold_offset<true> in u32 arithmetic."""
-    go = (8 * int(idx) - 8 * (nh + 1)) & 0xFFFFFFFF
-    t = min(int(go) >> (PIECE_SHIFT + 3), PIECE_TBL)
-    return (int(go) + int(tbl[x, t])) & 0xFFFFFFFF
+def cold_offset(shim, idx, x, tbl, nh):
+    """pr_spmv.h cold_offset<true> (pr_pieces.h piece_cold_offset) in u32 arithmetic."""
+    a, out = np.array([idx], np.uint32), np.zeros(1, np.uint32)
+    t = np.ascontiguousarray(tbl[x])
+    shim.prp_cold_offset(_p(a), 1, nh, _p(t), _p(out))
+    return int(out[0])
 
 
 @pytest.mark.parametrize("P,C,seed", [(2, 16, 0), (3, 32, 1), (8, 32, 2), (8, 64, 3), (4, 8, 4)])
-def test_piece_codes_round_trip(P, C, seed):
+def test_piece_codes_round_trip(shim, P, C, seed):
     rng = np.random.default_rng(seed)
     Q = int(rng.integers(2000, 40000))  # class region rows of a slice
     S = C * Q + 2
@@ -80,7 +94,7 @@ def test_piece_codes_round_trip(P, C, seed):
                 base += n
         if p != self_part:
             base += 2  # the run's two slots (no class's sources)
-    pc, tbl, vmax = plan_pieces(lo, hi)
+    pc, tbl, vmax = plan_pieces(shim, lo, hi)
     nh = 18299 // P * P
     assert nh + vmax < (1 << 20)
     gather_bytes = 8 * base
@@ -90,22 +104,22 @@ def test_piece_codes_round_trip(P, C, seed):
             if len(m) == 0:
                 continue
             for pos in rng.choice(m, size=min(64, len(m)), replace=False).tolist() + [int(m[0]), int(m[-1])]:
-                idx = encode(pos, 0, x, pc, nh)
+                idx = encode(shim, pos, 0, x, pc, nh)
                 assert nh < idx < (1 << 20)
-                assert cold_offset(idx, x, tbl, nh) == 8 * pos
+                assert cold_offset(shim, idx, x, tbl, nh) == 8 * pos
         # hot slots and padding (idx 0) stay out of range, and their LDS read is the slot itself
         for idx in [0, 1, nh // 2, nh]:
-            off = cold_offset(idx, x, tbl, nh)
+            off = cold_offset(shim, idx, x, tbl, nh)
             assert off >= (1 << 31) and off >= gather_bytes
             assert min(8 * idx, 8 * (nh + 1)) == 8 * idx
         # a cold entry's LDS read is clamped to the zero slot
         assert min(8 * (nh + 1 + 5), 8 * (nh + 1)) == 8 * (nh + 1)
 
 
-def test_piece_plan_alignment_and_table_ownership():
+def test_piece_plan_alignment_and_table_ownership(shim):
     lo = np.array([[0, 100000, 0], [5000, 200000, 300000]], np.int64)
     hi = np.array([[4097, 100001, 0], [9000, 200000, 309999]], np.int64)
-    pc, tbl, vmax = plan_pieces(lo, hi)
+    pc, tbl, vmax = plan_pieces(shim, lo, hi)
     # class 0: pieces at virtual 0 (4097 long -> blocks 0, 1) and 8192 (1 long); part 2 empty
     assert pc[0, 0].tolist() == [0, 4097, 0] and pc[0, 1].tolist() == [100000, 100001, 8192]
     assert vmax == 4096 + 9999  # class 1: 4000 rows, then 9999 from the next boundary
