@@ -288,7 +288,6 @@ int pr_get_ranks(pr_graph *g, double *ranks_out) {
 int pr_set_timing(pr_graph *g, int32_t enable) {
   if (!g) return fail(PR_ERR_INVALID, "NULL graph");
   g->timing = enable != 0;
-  if (!g->timing) g->overlap_start_ev = -1;
   return PR_OK;
 }
 
@@ -515,17 +514,12 @@ void pr_graph_destroy(pr_graph *g) {
   DeviceGuard dg(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->xstream) (void)hipStreamSynchronize(g->xstream);
-  if (g->estream) (void)hipStreamSynchronize(g->estream);
   if (g->comm) (void)ncclCommDestroy(g->comm);
   for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
   if (g->xev) (void)hipEventDestroy(g->xev);
   for (hipEvent_t e : g->x_ev) (void)hipEventDestroy(e);
   if (g->x_pack_ev) (void)hipEventDestroy(g->x_pack_ev);
   if (g->xstream) (void)hipStreamDestroy(g->xstream);
-  for (hipEvent_t e : g->e_chunk) (void)hipEventDestroy(e);
-  if (g->e_hot) (void)hipEventDestroy(g->e_hot);
-  if (g->e_fin) (void)hipEventDestroy(g->e_fin);
-  if (g->estream) (void)hipStreamDestroy(g->estream);
   g->ev_pool.clear();
   hipStream_t s = g->stream;
   g->stream = nullptr;

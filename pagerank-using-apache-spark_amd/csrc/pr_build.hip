@@ -817,14 +817,14 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                                                      : kCodeU32;
       if (code_is_piece(g->code)) slots = ps;
     }
-    // epilogue overlap: the hot set leaves LDS room for two one-wave epilogue workgroups per CU
-    // (their 8 KiB windows, rounded up to 1 KiB allocation blocks)
-    const bool overlap = g->opts.epi_overlap && P == 1 && C >= 2 * kXcds && C <= kWave;
+    // epilogue overlap (k_spmv_hot_epi): one part, compact codes, 16..64 classes; the hot set
+    // leaves LDS room for the epilogue waves' windows
+    const bool overlap = g->opts.epi_overlap && P == 1 && C >= 2 * kXcds && C <= kWave &&
+                         (g->code == kCodeC20 || g->code == kCodeC24);
     if (overlap) {
       HotGeom t{};
       t.P = 1;
-      const size_t epi = 2 * ((epi_grp_lds(true) + 1023) & ~size_t(1023));
-      for (t.Kp = slots; t.Kp > 0 && t.lds_bytes() + epi > (size_t)kHotLdsBytes; --t.Kp) {
+      for (t.Kp = slots; t.Kp > 0 && hot_epi_lds(t) > (size_t)kHotLdsBytes; --t.Kp) {
       }
       slots = t.Kp;
     }
@@ -977,26 +977,18 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     g->epi_narrow = epi_narrow_ok(C) && (g->opts.epi_narrow < 0 ? auto_narrow : g->opts.epi_narrow != 0);
     g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
   }
-  int64_t ep_parts = g->ep_blocks;
+  // the split epilogue writes one {dangling, L1} partial per group (pr_spmv.h epi_group)
+  const int64_t ep_parts = C > 1 ? (g->nblk + kEpiGroup - 1) / kEpiGroup : 0;
   if (g->epi_overlap) {
     // chunk c = the rows of class regions [8c, 8c + 8): Q_pad / 64 groups of 8 blocks (Q_pad is a
     // multiple of 64, so chunks start on group boundaries)
     g->n_echunks = n_hot_phases(g);
     g->ep_chunk_groups = g->Q_pad / kWave;
-    if (g->ep_chunk_groups * g->n_echunks != (g->nblk + kEpiGroup - 1) / kEpiGroup)
+    if (g->n_echunks < 2 || g->ep_chunk_groups * g->n_echunks != ep_parts)
       return fail(PR_ERR_STATE, "epilogue chunks do not tile the groups");
-    int n_cu = 0;
-    PR_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device));
     g->ep_blocks0 = (int)grid_for(g->ep_chunk_groups, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
-    g->ep_thin = 2 * n_cu;
-    ep_parts = std::max<int64_t>(ep_parts, g->ep_blocks0 + (int64_t)(g->n_echunks - 1) * g->ep_thin);
-    PR_HIP(hipStreamCreateWithFlags(&g->estream, hipStreamNonBlocking));
-    g->e_chunk.assign(g->n_echunks, nullptr);
-    for (auto &e : g->e_chunk) PR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    PR_HIP(hipEventCreateWithFlags(&g->e_hot, hipEventDisableTiming));
-    PR_HIP(hipEventCreateWithFlags(&g->e_fin, hipEventDisableTiming));
   }
-  // finalize input: fused-unit partials (C = 1) or the split epilogue's block partials (C > 1)
+  // finalize input: fused-unit partials (C = 1) or the split epilogue's group partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + ep_parts + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));
 

@@ -102,22 +102,21 @@ struct pr_graph {
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   int64_t hot_cover_ppm = 0;  // in-links whose source is in a class's hot set (layout policy input)
   pr::DevBuf cbuf[2];
-  // Epilogue overlap (PR_BOPT_EPI_OVERLAP, pr_iter.hip): the epilogue of iteration i runs on
-  // estream in n_echunks chunks of ep_chunk_groups epilogue groups -- chunk c = the rows of the
-  // class regions hot phase c reads -- and phase c of iteration i + 1 waits only for e_chunk[c].
-  // The hot kernel of i + 1 writes the other partial buffer (partial / partial2, pbuf) while the
-  // epilogue of i reads this one.  Chunk 0 (alone on the critical path) uses the full grid, the
-  // others ep_thin one-wave workgroups, two per CU beside k_spmv_hot's workgroup.
+  // Epilogue overlap (PR_BOPT_EPI_OVERLAP, pr_iter.hip iter_compute_overlap): the epilogue of
+  // iteration i is cut into n_echunks chunks of ep_chunk_groups groups -- chunk c = the rows of the
+  // class regions hot phase c reads.  Chunk 0 runs alone after the hot pass (ep_blocks0
+  // workgroups); chunk c >= 1 runs inside the launch of hot phase c - 1 of iteration i + 1
+  // (k_spmv_hot_epi), and the finalize of i before phase n_echunks - 1.  The hot pass of i + 1
+  // writes the other partial buffer (partial / partial2, pbuf) while the epilogue of i reads this
+  // one.  epi_pending: chunks >= 1 and the finalize of the last iteration (pend_*) are not launched
+  // yet; join_exchange launches them before anything reads ranks, slots or contributions.
   bool epi_overlap = false;
   int pbuf = 0;
   pr::DevBuf partial2;
-  hipStream_t estream = nullptr;
-  std::vector<hipEvent_t> e_chunk;
-  hipEvent_t e_hot = nullptr, e_fin = nullptr;
-  bool epi_pending = false;  // estream holds an epilogue the compute stream has not joined
-  int n_echunks = 0, ep_blocks0 = 0, ep_thin = 0;
+  bool epi_pending = false;
+  int pend_in = 0, pend_out = 0, pend_pbuf = 0;
+  int n_echunks = 0, ep_blocks0 = 0;
   int64_t ep_chunk_groups = 0;
-  int overlap_start_ev = -1;  // timing: where the next pass interval starts (ev_pool index)
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;
   pr::DevBuf fin_part, fin_counter;

@@ -179,6 +179,11 @@ int prepare_hot_kernel() {
         PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
+  for (int code : {kCodeC20, kCodeC24})
+    for (int c : {16, 32, 64})
+      for (bool walk : {false, true})
+        PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hot_epi_kernel(code, c, walk)),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
                         reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>),
                         reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>),
@@ -264,11 +269,10 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
 
 void set_exchange_chunking(pr_graph *g) { g->x_chunked = g->opts.xchg_chunks && g->n_xc > 1; }
 
+int flush_epilogue(pr_graph *g);
+
 int join_exchange(pr_graph *g) {
-  if (g->epi_pending) {  // the overlapped epilogue (and its finalize) still on estream
-    PR_HIP(hipStreamWaitEvent(g->stream, g->e_fin, 0));
-    g->epi_pending = false;
-  }
+  PR_TRY(flush_epilogue(g));  // the overlapped epilogue's deferred chunks and finalize
   if (!g->x_pending) return PR_OK;
   PR_HIP(hipStreamWaitEvent(g->stream, g->x_ev.back(), 0));  // chunks are recorded in order
   g->x_pending = false;
@@ -289,7 +293,6 @@ int iter_reset(pr_graph *g, const double *init_host) {
   }
   g->cur = 0;
   g->pbuf = 0;
-  g->overlap_start_ev = -1;
   g->x_packed = -1;
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
@@ -313,60 +316,99 @@ int iter_reset(pr_graph *g, const double *init_host) {
 }
 
 // The epilogue overlapped with the next iteration's hot phases (PR_BOPT_EPI_OVERLAP; P = 1, split
-// layout).  Compute stream: hot phase c of this iteration waits for chunk c of the previous
-// epilogue (the contributions of the class regions it reads), then k_seg_reduce.  estream: the
-// epilogue of this iteration in chunks, chunk c recorded as e_chunk[c], then k_finalize.  The hot
-// kernel writes the partial buffer the running epilogue does not read (pbuf flips per iteration);
-// everything an epilogue reads or writes besides -- r, c' of its chunk's rows, the dc slots -- no
-// hot phase touches, and estream runs the epilogues and finalizes in iteration order.  Timing: one
-// interval per pass, from the previous pass's finalize (the first: this pass's phase 0) to this
-// finalize, so the intervals tile the timed run.
+// layout, compact codes).  One stream; iteration i launches
+//   phase 0 of i + epilogue chunk 1 of i - 1    (k_spmv_hot_epi)
+//   ...
+//   phase n-2 of i + epilogue chunk n-1 of i - 1
+//   k_finalize of i - 1                          (dc for the epilogue of i)
+//   phase n-1 of i                               (k_spmv_hot)
+//   k_seg_reduce of i
+//   epilogue chunk 0 of i                        (k_epilogue_grp: phase 0 of i + 1 reads its rows)
+// and leaves chunks 1.. and the finalize of i pending.  Hot phase c reads only the contributions of
+// class regions 8c .. 8c + 7 = epilogue chunk c's rows, written before it in stream order; the hot
+// phases of i write one partial buffer while the epilogue chunks of i - 1 read the other (pbuf);
+// an epilogue chunk writes r and c' of its own rows only.  join_exchange launches what is pending.
+// Timing: one interval per iteration, its first launch to its chunk 0 (the flush of the last
+// iteration's remaining chunks extends the last interval), so the intervals tile the run.
+namespace {
+int launch_epi_range(pr_graph *g, int64_t g0, int64_t g1, int pb, int in, int out) {
+  const int64_t gpc = g->ep_chunk_groups;
+  const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
+  const unsigned blocks = (unsigned)((int64_t)g->ep_blocks0 * ((g1 - g0 + gpc - 1) / gpc));
+  const double *part = (pb ? g->partial2 : g->partial).as<double>();
+  hipLaunchKernelGGL(epi, dim3(blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), g->stream,
+                     g->nblk, g0, g1, part, g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                     g->r.as<double>(), g->cbuf[out].as<double>() + g->own_off, g->cbuf[in].as<double>(), g->slots,
+                     (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
+                     g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(),
+                     PackDst{});
+  PR_HIP(hipGetLastError());
+  return PR_OK;
+}
+int64_t epi_groups(const pr_graph *g) { return (g->nblk + kEpiGroup - 1) / kEpiGroup; }
+}  // namespace
+
+int flush_epilogue(pr_graph *g) {
+  if (!g->epi_pending) return PR_OK;
+  g->epi_pending = false;
+  PR_TRY(launch_epi_range(g, g->ep_chunk_groups, epi_groups(g), g->pend_pbuf, g->pend_in, g->pend_out));
+  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + epi_groups(g), g->pend_in,
+                         g->pend_out, g->stream));
+  if (g->timing && !g->spmv_ev.empty()) {  // the deferred chunks belong to the last timed iteration
+    int e = -1;
+    PR_TRY(time_mark(g, g->stream, &e));
+    g->spmv_ev.back().second = e;
+    if (!g->iter_ev.empty()) g->iter_ev.back().second = e;
+  }
+  return PR_OK;
+}
+
 int iter_compute_overlap(pr_graph *g) {
-  hipStream_t s = g->stream, es = g->estream;
+  hipStream_t s = g->stream;
   const int in = g->cur, out = g->cur ^ 1;
   const int nph = n_hot_phases(g);
-  double *part = partial_buf(g);
+  int e0 = -1, e1 = -1;
+  if (g->timing) PR_TRY(time_mark(g, s, &e0));
+  const bool pend = g->epi_pending;
+  g->epi_pending = false;
+  const HotEpiFn fused = hot_epi_kernel(g->code, g->C, g->epi_walk);
+  if (!fused) return fail(PR_ERR_STATE, "no fused hot + epilogue kernel for this layout");
+  const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
+  const EpiArgs ea{g->nblk, (g->pend_pbuf ? g->partial2 : g->partial).as<double>(), g->rmask.p, g->cbase.as<int32_t>(),
+                   g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[g->pend_out].as<double>() + g->own_off,
+                   g->teleport, g->damping, g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
+                   g->x_sbase.as<int32_t>()};
   for (int c = 0; c < nph; ++c) {
-    if (g->epi_pending) PR_HIP(hipStreamWaitEvent(s, g->e_chunk[c], 0));
-    if (c == 0 && g->timing && g->overlap_start_ev < 0) PR_TRY(time_mark(g, s, &g->overlap_start_ev));
-    if (g->n_hunits > 0) PR_TRY(launch_hot(g, in, c, c + 1));
+    if (pend && c + 1 < g->n_echunks) {
+      const int64_t g0 = (int64_t)(c + 1) * g->ep_chunk_groups;
+      hipLaunchKernelGGL(fused, dim3((unsigned)g->hot_grid), dim3(kHotThreads), hot_epi_lds(g->hot), s,
+                         g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
+                         partial_buf(g), g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), c, ea,
+                         g->cbuf[g->pend_in].as<double>(), g->slots, (double)g->V, g0, g0 + g->ep_chunk_groups,
+                         g->unit_part.as<double2>() + g->n_units, PackDst{});
+      PR_HIP(hipGetLastError());
+      if (c + 1 == g->n_echunks - 1)  // the last chunk of i - 1 is out: its finalize (dc of i)
+        PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + epi_groups(g), g->pend_in,
+                               g->pend_out, s));
+    } else {
+      PR_TRY(launch_hot(g, in, c, c + 1));
+    }
   }
   if (g->n_segs > 0)
     hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
-                       g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(), part);
-  PR_HIP(hipEventRecord(g->e_hot, s));
-  PR_HIP(hipStreamWaitEvent(es, g->e_hot, 0));
-  const int64_t own = g->own_off;
-  double2 *ep_part = g->unit_part.as<double2>() + g->n_units;
-  int64_t n_parts = 0;
-  for (int c = 0; c < g->n_echunks; ++c) {
-    const bool fat = c == 0;  // alone on the critical path: the full grid
-    const bool narrow = fat ? g->epi_narrow : true;
-    const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, narrow);
-    const int blocks = fat ? g->ep_blocks0 : g->ep_thin;
-    const int64_t g0 = (int64_t)c * g->ep_chunk_groups;
-    hipLaunchKernelGGL(epi, dim3(blocks), dim3(epi_grp_threads(narrow)), epi_grp_lds(narrow), es, g->nblk, g0,
-                       g0 + g->ep_chunk_groups, part, g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
-                       g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
-                       (double)g->V, g->teleport, g->damping, ep_part + n_parts, g->eoff.as<int64_t>(),
-                       g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(), PackDst{});
-    n_parts += blocks;
-    PR_HIP(hipEventRecord(g->e_chunk[c], es));
-  }
-  PR_HIP(hipGetLastError());
-  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + n_parts, in, out, es));
-  PR_HIP(hipEventRecord(g->e_fin, es));
-  if (g->timing) {
-    int e = -1;
-    PR_TRY(time_mark(g, es, &e));
-    g->spmv_ev.push_back({g->overlap_start_ev, e});
-    g->iter_ev.push_back({g->overlap_start_ev, e});
-    ++g->spmv_passes;
-    g->overlap_start_ev = e;
-  } else {
-    g->overlap_start_ev = -1;
-  }
+                       g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
+                       partial_buf(g));
+  PR_TRY(launch_epi_range(g, 0, g->ep_chunk_groups, g->pbuf, in, out));
   g->epi_pending = true;
+  g->pend_in = in;
+  g->pend_out = out;
+  g->pend_pbuf = g->pbuf;
+  if (g->timing) {
+    PR_TRY(time_mark(g, s, &e1));
+    g->spmv_ev.push_back({e0, e1});
+    g->iter_ev.push_back({e0, e1});
+    ++g->spmv_passes;
+  }
   g->pbuf ^= 1;
   g->cur = out;
   ++g->iters_done;
@@ -445,7 +487,7 @@ int iter_compute(pr_graph *g) {
                        (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
                        g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
                        g->x_sbase.as<int32_t>(), pd);
-    n_parts += g->ep_blocks;
+    n_parts += epi_groups(g);
   }
   PR_HIP(hipGetLastError());
   PR_TRY(mark_end());

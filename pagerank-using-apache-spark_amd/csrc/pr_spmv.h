@@ -642,6 +642,43 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   }
 }
 
+// Stage class x's hot contributions (the previous iteration's, final before this launch) into LDS
+// slots 1..nh, the 0.0 slots and the workgroup's unit counter (all 1024 threads; the caller's
+// barrier follows): every position load, then every gather in flight before the first LDS write --
+// a rolled loop pays two dependent memory latencies per element, 18 times per phase (-2.7 % at s26).
+template <bool PIECE>
+__device__ __forceinline__ void stage_hot_set(const HotGeom &hg, int x, const int32_t *__restrict__ hpos,
+                                              const int32_t *__restrict__ ptab, const double *__restrict__ cin,
+                                              double *hot, uint32_t *tblw) {
+  const int nh = hg.P * hg.Kp;
+  const int32_t *hp = hpos + (int64_t)x * nh;
+  constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18429 slots)
+  for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
+    int32_t pos[kSB];
+    double val[kSB];
+#pragma unroll
+    for (int j = 0; j < kSB; ++j) {
+      const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+      pos[j] = i < nh ? hp[i] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < kSB; ++j) val[j] = pos[j] >= 0 ? cin[pos[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < kSB; ++j) {
+      const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+      if (i < nh) hot[1 + i] = val[j];
+    }
+  }
+  if constexpr (PIECE)
+    for (int i = (int)threadIdx.x; i < kPieceTblWords; i += kHotThreads)
+      tblw[i] = (uint32_t)ptab[(int64_t)x * kPieceTblWords + i];
+  if (threadIdx.x == 0) {
+    hot[0] = 0.0;
+    hot[hg.slots()] = 0.0;
+    *reinterpret_cast<uint32_t *>(hot + hg.ctr_slot()) = 0u;  // the workgroup's unit counter
+  }
+}
+
 // The class units of the split layout, one 1024-thread workgroup per CU (a grid that is a
 // multiple of the XCD count).  All of an XCD's workgroups run its classes one after another
 // (phases [ph0, ph1): one launch per phase when the exchange overlaps), restaging the hot set
@@ -657,7 +694,6 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           const int32_t *__restrict__ hpos,
                                                           const int32_t *__restrict__ ptab, int ph0, int ph1) {
   extern __shared__ double hot[];
-  const int nh = hg.P * hg.Kp;
   constexpr bool kPiece = code_is_piece(CODE);
   ClassSrc cs;
   cs.zb = (uint32_t)hg.slots() * 8u;
@@ -677,35 +713,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                  (uint32_t)((hg.Q_pad - hg.q_load) * 8), 0x00020000);
     }
     if (ph > ph0) __syncthreads();  // every wave is done with the previous class's hot set
-    // stage the class's hot contributions (the previous iteration's, final before this launch):
-    // every position load, then every gather in flight before the first LDS write -- a rolled
-    // loop pays two dependent memory latencies per element, 18 times per phase (-2.7 % at s26)
-    const int32_t *hp = hpos + (int64_t)x * nh;
-    constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18429 slots)
-    for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
-      int32_t pos[kSB];
-      double val[kSB];
-#pragma unroll
-      for (int j = 0; j < kSB; ++j) {
-        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
-        pos[j] = i < nh ? hp[i] : -1;
-      }
-#pragma unroll
-      for (int j = 0; j < kSB; ++j) val[j] = pos[j] >= 0 ? cin[pos[j]] : 0.0;
-#pragma unroll
-      for (int j = 0; j < kSB; ++j) {
-        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
-        if (i < nh) hot[1 + i] = val[j];
-      }
-    }
-    if constexpr (kPiece)
-      for (int i = (int)threadIdx.x; i < kPieceTblWords; i += kHotThreads)
-        tblw[i] = (uint32_t)ptab[(int64_t)x * kPieceTblWords + i];
-    if (threadIdx.x == 0) {
-      hot[0] = 0.0;
-      hot[hg.slots()] = 0.0;
-      *reinterpret_cast<uint32_t *>(hot + hg.ctr_slot()) = 0u;  // the workgroup's unit counter
-    }
+    stage_hot_set<kPiece>(hg, x, hpos, ptab, cin, hot, tblw);
     __syncthreads();
     hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
   }
@@ -786,6 +794,213 @@ __device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
 // class order -- as many steps per block as its busiest row has classes, instead of one per class
 // -- and the sums are bitwise those of the class loop (whose absent classes add an exact +0).
 // (at least 4 waves per SIMD: the LDS of four four-wave workgroups per CU)
+
+// The arguments of the grouped epilogue (k_epilogue_grp, k_spmv_hot_epi); the fused-pack target
+// (an array indexed by peer) stays a kernel argument, passed on by reference (a local copy of it
+// would be indexed in scratch).
+struct EpiArgs {
+  int64_t nblk;
+  const double *partial;
+  const void *rmask;
+  const int32_t *cbase;
+  const uint32_t *rowinfo;
+  double *r, *cout;
+  double teleport, damping;
+  const int64_t *eoff;
+  const uint16_t *epos;
+  const uint8_t *pmask;
+  const int32_t *sbase;
+};
+
+// One group gi (kEpiGroup consecutive 64-row blocks) of the grouped epilogue, by one wave with its
+// LDS window win (kEpiWin slots + the zero slot win[kEpiWin]).  The group's dangling and L1
+// partials go to ep_part[gi] (a fixed-order wave sum), so k_finalize adds the same values in the
+// same order whichever wave, workgroup or launch ran the group: every epilogue schedule (one
+// pass, chunks on a second stream, epilogue waves inside k_spmv_hot_epi) is bitwise the same.
+// The body of k_epilogue_grp (below) and of k_spmv_hot_epi's epilogue waves.
+template <int C, bool WALK>
+__device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, int64_t gi, double tdc, double *win,
+                                          double2 *__restrict__ ep_part) {
+  double dcp = 0.0, l1p = 0.0;
+  constexpr int G = kEpiGroup, W = kEpiWin;
+  constexpr int MW = mask_words<C>();  // 32-bit mask words per row
+  static_assert(MW == 1 || MW == 2 || MW == 4, "mask words");
+  static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
+  static_assert(!WALK || C <= kWave, "the per-row walk needs at most 64 classes");
+  const int lane = lane_id();
+  const int64_t b0 = gi * G;
+  const int nb = (int)min((int64_t)G, a.nblk - b0);
+  uint32_t mw[MW][G], info[G];
+  double rold[G], S[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t L = (b0 + g) * kWave + lane;
+    const bool ok = g < nb;
+    if constexpr (MW == 4) {
+      const uint4 q = ok ? static_cast<const uint4 *>(a.rmask)[L] : make_uint4(0u, 0u, 0u, 0u);
+      mw[0][g] = q.x, mw[1][g] = q.y, mw[2][g] = q.z, mw[3][g] = q.w;
+    } else if constexpr (MW == 2) {
+      const uint2 q = ok ? static_cast<const uint2 *>(a.rmask)[L] : make_uint2(0u, 0u);
+      mw[0][g] = q.x, mw[1][g] = q.y;
+    } else {
+      mw[0][g] = ok ? static_cast<const uint32_t *>(a.rmask)[L] : 0u;
+    }
+    info[g] = ok ? a.rowinfo[L] : kRowHole;
+    rold[g] = ok ? a.r[L] : 0.0;
+    S[g] = 0.0;
+  }
+  // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
+  // per class with v_readlane
+  const int cs = lane < C ? a.cbase[b0 * C + lane] : 0;
+  const int ce = lane < C ? a.cbase[(b0 + nb) * C + lane] : 0;
+  if constexpr (C <= kWave) {
+    // lane y: class y's run start rounded down to 16 bytes (sa), its staged length n2 (0: no
+    // slots in this group) and its window position, the exclusive prefix of n2 over the
+    // classes.  A batch is the longest sequence of classes from x0 whose staged runs fit the
+    // window (one ballot), so the per-class work is a readlane or two and the DMA itself.
+    const int sa = cs & ~1;
+    const int n2 = (lane < C && ce > cs) ? (((ce + 1) & ~1) - sa) : 0;
+    const int incl = wave_incl_scan_i32(n2);
+    const int pre = incl - n2;
+    const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
+    bool walked = false;
+    if constexpr (WALK) {
+      const int64_t eo = a.eoff[gi];
+      if (eo >= 0) {  // one batch: every class's run and every slot's position fit the window
+        const int nsl = lane < C ? ce - cs : 0;  // class y's slots in this group
+        const int sincl = wave_incl_scan_i32(nsl);
+        for (int y = 0; y < C; ++y) {
+          const int n = __builtin_amdgcn_readlane(n2, y);
+          if (n == 0) continue;
+          const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
+          double *dst = win + __builtin_amdgcn_readlane(pre, y);
+          for (int o = 0; o < n; o += 2 * kWave)
+            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+        }
+        const int Tb = __builtin_amdgcn_readlane(incl, C - 1);  // staged slots (even)
+        const int nl = (__builtin_amdgcn_readlane(sincl, C - 1) + 7) >> 3;  // 16-byte lanes of positions
+        const double *esrc = reinterpret_cast<const double *>(a.epos + eo);
+        for (int o = 0; o < nl; o += kWave)
+          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
+        const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
+        int acc = 0;  // index of block g's first position
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const uint64_t m = (uint64_t)(MW > 1 ? mw[MW > 1 ? 1 : 0][g] : 0u) << 32 | mw[0][g];
+          const int cnt = __popcll(m);
+          const int inc = wave_incl_scan_i32(cnt);
+          const uint16_t *e = ep + acc + inc - cnt;  // this row's positions, in class order
+          acc += __builtin_amdgcn_readlane(inc, kWave - 1);
+          for (int k = 0; __ballot(k < cnt) != 0ull; ++k)
+            if (k < cnt) S[g] = __dadd_rn(S[g], win[e[k]]);
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next group's DMA
+        walked = true;
+      }
+    }
+    for (int x0 = 0; x0 < C && !walked;) {
+      const int base = __builtin_amdgcn_readlane(pre, x0);
+      const unsigned long long over = __ballot(lane >= x0 && lane < C && incl - base > W);
+      const int x1 = over ? (int)__builtin_ctzll(over) : C;  // > x0: one run always fits
+      for (int y = x0; y < x1; ++y) {
+        const int n = __builtin_amdgcn_readlane(n2, y);
+        if (n == 0) continue;
+        const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
+        double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
+        for (int o = 0; o < n; o += 2 * kWave)
+          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
+      for (int y = x0; y < x1; ++y) {
+        if (__builtin_amdgcn_readlane(n2, y) == 0) continue;
+        const uint32_t bit = 1u << (y & 31);
+        const int run = __builtin_amdgcn_readlane(roff, y) - base;
+        if (MW == 1 || y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
+        else epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+      x0 = x1;
+    }
+  } else {  // 128 classes: lanes 64..127's class runs come from a second register
+    const int cs1 = lane + kWave < C ? a.cbase[b0 * C + kWave + lane] : 0;
+    const int ce1 = lane + kWave < C ? a.cbase[(b0 + nb) * C + kWave + lane] : 0;
+    auto run_start = [&](int y) {
+      return y < kWave ? __builtin_amdgcn_readlane(cs, y) : __builtin_amdgcn_readlane(cs1, y - kWave);
+    };
+    auto run_end = [&](int y) {
+      return y < kWave ? __builtin_amdgcn_readlane(ce, y) : __builtin_amdgcn_readlane(ce1, y - kWave);
+    };
+    for (int x = 0; x < C;) {
+      // stage the runs of classes [x, xe) that fit the window (at least one always does)
+      int fill = 0, xe = x;
+      for (; xe < C; ++xe) {
+        const int s = run_start(xe), e = run_end(xe);
+        if (e == s) continue;  // no slots in this group
+        const int sa = s & ~1, n2 = ((e + 1) & ~1) - sa;
+        if (xe > x && fill + n2 > W) break;
+        const double *src = a.partial + sa;
+        for (int o = 0; o < n2; o += 2 * kWave)
+          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
+        fill += n2;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
+      fill = 0;
+      for (int y = x; y < xe; ++y) {
+        const int s = run_start(y), e = run_end(y);
+        if (e == s) continue;
+        const int sa = s & ~1;
+        const uint32_t bit = 1u << (y & 31);
+        const int run = fill + (s - sa);
+        // static word index (a runtime index into mw would put it in scratch)
+        if (y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
+        else if (y < 64) epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
+        else if (y < 96) epi_class_add<G>(mw[MW > 2 ? 2 : 0], bit, run, win, W, S);
+        else epi_class_add<G>(mw[MW > 3 ? 3 : 0], bit, run, win, W, S);
+        fill += ((e + 1) & ~1) - sa;
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
+      x = xe;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t L = (b0 + g) * kWave + lane;
+    double Sv = S[g];
+    uint32_t any = 0u;
+#pragma unroll
+    for (int w = 0; w < MW; ++w) any |= mw[w][g];
+    if (any == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
+    const double rn = affine(Sv, tdc, a.teleport, a.damping);
+    double cn = 0.0;
+    if (!(info[g] & kRowHole)) {
+      a.r[L] = rn;
+      const uint32_t d = info[g] & kRowDegMask;
+      if (d > 0) {
+        cn = __ddiv_rn(rn, (double)d);
+        a.cout[L] = cn;
+      } else if (info[g] & kRowSink) {
+        dcp = __dadd_rn(dcp, rn);
+      }
+      l1p = __dadd_rn(l1p, fabs(rn - rold[g]));
+    }
+    if (pd.P > 1 && g < nb) {  // fused pack: c' into the send run of every peer that reads the row
+      const uint32_t pm = a.pmask[L];
+      const int64_t sb = (b0 + g) * pd.P;
+      for (int q = 0; q < pd.P; ++q) {
+        const bool has = (pm >> q) & 1u;
+        const unsigned long long bal = __ballot(has);
+        if (bal == 0ull) continue;
+        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (has) pd.sbuf[pd.soff[q] + a.sbase[sb + q] + k] = cn;
+      }
+    }
+  }
+  dcp = wave_sum(dcp);
+  l1p = wave_sum(l1p);
+  if (lane == 0) ep_part[gi] = make_double2(dcp, l1p);
+}
+
 //
 // Groups [g_lo, g_hi) only: the whole pass, or one chunk of the overlapped epilogue (PR_BOPT_EPI_OVERLAP).
 template <int C, bool WALK, int NT>
@@ -793,196 +1008,84 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
     int64_t nblk, int64_t g_lo, int64_t g_hi, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
-    double damping, double2 *__restrict__ ep_part, const int64_t *__restrict__ eoff,
+    double damping, double2 *__restrict__ ep_part /* [group] */, const int64_t *__restrict__ eoff,
     const uint16_t *__restrict__ epos, const uint8_t *__restrict__ pmask, const int32_t *__restrict__ sbase,
     PackDst pd) {
-  constexpr int G = kEpiGroup, W = kEpiWin;
+  constexpr int W = kEpiWin;
   constexpr int NW = NT / kWave;
-  constexpr int MW = mask_words<C>();  // 32-bit mask words per row
-  static_assert(MW == 1 || MW == 2 || MW == 4, "mask words");
-  static_assert(W >= 64 * G + 2, "one class run of a group must fit the window");
-  static_assert(!WALK || C <= kWave, "the per-row walk needs at most 64 classes");
-  extern __shared__ double epi_lds[];  // NW windows of W + 2 slots, then NW double2 for the block sum
+  extern __shared__ double epi_lds[];  // NW windows of W + 2 slots
+  const EpiArgs a{nblk, partial, rmask_v, cbase, rowinfo, r, cout, teleport, damping, eoff, epos, pmask, sbase};
   const int lane = lane_id();
   const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *win = epi_lds + wv * (W + 2);
   if (lane == 0) win[W] = 0.0;  // the zero slot (never a DMA target: fill <= W)
   const double tdc = dc_from_slots(cin, sp) / n_vertices;
-  double dcp = 0.0, l1p = 0.0;
   const int64_t nw = (int64_t)gridDim.x * NW;
-  for (int64_t gi = g_lo + (int64_t)blockIdx.x * NW + wv; gi < g_hi; gi += nw) {
-    const int64_t b0 = gi * G;
-    const int nb = (int)min((int64_t)G, nblk - b0);
-    uint32_t mw[MW][G], info[G];
-    double rold[G], S[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int64_t L = (b0 + g) * kWave + lane;
-      const bool ok = g < nb;
-      if constexpr (MW == 4) {
-        const uint4 q = ok ? static_cast<const uint4 *>(rmask_v)[L] : make_uint4(0u, 0u, 0u, 0u);
-        mw[0][g] = q.x, mw[1][g] = q.y, mw[2][g] = q.z, mw[3][g] = q.w;
-      } else if constexpr (MW == 2) {
-        const uint2 q = ok ? static_cast<const uint2 *>(rmask_v)[L] : make_uint2(0u, 0u);
-        mw[0][g] = q.x, mw[1][g] = q.y;
-      } else {
-        mw[0][g] = ok ? static_cast<const uint32_t *>(rmask_v)[L] : 0u;
-      }
-      info[g] = ok ? rowinfo[L] : kRowHole;
-      rold[g] = ok ? r[L] : 0.0;
-      S[g] = 0.0;
-    }
-    // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
-    // per class with v_readlane
-    const int cs = lane < C ? cbase[b0 * C + lane] : 0;
-    const int ce = lane < C ? cbase[(b0 + nb) * C + lane] : 0;
-    if constexpr (C <= kWave) {
-      // lane y: class y's run start rounded down to 16 bytes (sa), its staged length n2 (0: no
-      // slots in this group) and its window position, the exclusive prefix of n2 over the
-      // classes.  A batch is the longest sequence of classes from x0 whose staged runs fit the
-      // window (one ballot), so the per-class work is a readlane or two and the DMA itself.
-      const int sa = cs & ~1;
-      const int n2 = (lane < C && ce > cs) ? (((ce + 1) & ~1) - sa) : 0;
-      const int incl = wave_incl_scan_i32(n2);
-      const int pre = incl - n2;
-      const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
-      bool walked = false;
-      if constexpr (WALK) {
-        const int64_t eo = eoff[gi];
-        if (eo >= 0) {  // one batch: every class's run and every slot's position fit the window
-          const int nsl = lane < C ? ce - cs : 0;  // class y's slots in this group
-          const int sincl = wave_incl_scan_i32(nsl);
-          for (int y = 0; y < C; ++y) {
-            const int n = __builtin_amdgcn_readlane(n2, y);
-            if (n == 0) continue;
-            const double *src = partial + __builtin_amdgcn_readlane(sa, y);
-            double *dst = win + __builtin_amdgcn_readlane(pre, y);
-            for (int o = 0; o < n; o += 2 * kWave)
-              if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
-          }
-          const int Tb = __builtin_amdgcn_readlane(incl, C - 1);  // staged slots (even)
-          const int nl = (__builtin_amdgcn_readlane(sincl, C - 1) + 7) >> 3;  // 16-byte lanes of positions
-          const double *esrc = reinterpret_cast<const double *>(epos + eo);
-          for (int o = 0; o < nl; o += kWave)
-            if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
-          __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
-          const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
-          int acc = 0;  // index of block g's first position
-#pragma unroll
-          for (int g = 0; g < G; ++g) {
-            const uint64_t m = (uint64_t)(MW > 1 ? mw[MW > 1 ? 1 : 0][g] : 0u) << 32 | mw[0][g];
-            const int cnt = __popcll(m);
-            const int inc = wave_incl_scan_i32(cnt);
-            const uint16_t *e = ep + acc + inc - cnt;  // this row's positions, in class order
-            acc += __builtin_amdgcn_readlane(inc, kWave - 1);
-            for (int k = 0; __ballot(k < cnt) != 0ull; ++k)
-              if (k < cnt) S[g] = __dadd_rn(S[g], win[e[k]]);
-          }
-          __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next group's DMA
-          walked = true;
-        }
-      }
-      for (int x0 = 0; x0 < C && !walked;) {
-        const int base = __builtin_amdgcn_readlane(pre, x0);
-        const unsigned long long over = __ballot(lane >= x0 && lane < C && incl - base > W);
-        const int x1 = over ? (int)__builtin_ctzll(over) : C;  // > x0: one run always fits
-        for (int y = x0; y < x1; ++y) {
-          const int n = __builtin_amdgcn_readlane(n2, y);
-          if (n == 0) continue;
-          const double *src = partial + __builtin_amdgcn_readlane(sa, y);
-          double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
-          for (int o = 0; o < n; o += 2 * kWave)
-            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
-        }
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
-        for (int y = x0; y < x1; ++y) {
-          if (__builtin_amdgcn_readlane(n2, y) == 0) continue;
-          const uint32_t bit = 1u << (y & 31);
-          const int run = __builtin_amdgcn_readlane(roff, y) - base;
-          if (MW == 1 || y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
-          else epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
-        }
-        __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
-        x0 = x1;
-      }
-    } else {  // 128 classes: lanes 64..127's class runs come from a second register
-      const int cs1 = lane + kWave < C ? cbase[b0 * C + kWave + lane] : 0;
-      const int ce1 = lane + kWave < C ? cbase[(b0 + nb) * C + kWave + lane] : 0;
-      auto run_start = [&](int y) {
-        return y < kWave ? __builtin_amdgcn_readlane(cs, y) : __builtin_amdgcn_readlane(cs1, y - kWave);
-      };
-      auto run_end = [&](int y) {
-        return y < kWave ? __builtin_amdgcn_readlane(ce, y) : __builtin_amdgcn_readlane(ce1, y - kWave);
-      };
-      for (int x = 0; x < C;) {
-        // stage the runs of classes [x, xe) that fit the window (at least one always does)
-        int fill = 0, xe = x;
-        for (; xe < C; ++xe) {
-          const int s = run_start(xe), e = run_end(xe);
-          if (e == s) continue;  // no slots in this group
-          const int sa = s & ~1, n2 = ((e + 1) & ~1) - sa;
-          if (xe > x && fill + n2 > W) break;
-          const double *src = partial + sa;
-          for (int o = 0; o < n2; o += 2 * kWave)
-            if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
-          fill += n2;
-        }
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
-        fill = 0;
-        for (int y = x; y < xe; ++y) {
-          const int s = run_start(y), e = run_end(y);
-          if (e == s) continue;
-          const int sa = s & ~1;
-          const uint32_t bit = 1u << (y & 31);
-          const int run = fill + (s - sa);
-          // static word index (a runtime index into mw would put it in scratch)
-          if (y < 32) epi_class_add<G>(mw[0], bit, run, win, W, S);
-          else if (y < 64) epi_class_add<G>(mw[MW > 1 ? 1 : 0], bit, run, win, W, S);
-          else if (y < 96) epi_class_add<G>(mw[MW > 2 ? 2 : 0], bit, run, win, W, S);
-          else epi_class_add<G>(mw[MW > 3 ? 3 : 0], bit, run, win, W, S);
-          fill += ((e + 1) & ~1) - sa;
-        }
-        __builtin_amdgcn_s_waitcnt(0);  // the window's reads are done before the next DMA rewrites it
-        x = xe;
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int64_t L = (b0 + g) * kWave + lane;
-      double Sv = S[g];
-      uint32_t any = 0u;
-#pragma unroll
-      for (int w = 0; w < MW; ++w) any |= mw[w][g];
-      if (any == 0u) Sv = rold[g];  // no in-link: subtractByKey + union keeps the old rank (Sparky.java:224-225)
-      const double rn = affine(Sv, tdc, teleport, damping);
-      double cn = 0.0;
-      if (!(info[g] & kRowHole)) {
-        r[L] = rn;
-        const uint32_t d = info[g] & kRowDegMask;
-        if (d > 0) {
-          cn = __ddiv_rn(rn, (double)d);
-          cout[L] = cn;
-        } else if (info[g] & kRowSink) {
-          dcp = __dadd_rn(dcp, rn);
-        }
-        l1p = __dadd_rn(l1p, fabs(rn - rold[g]));
-      }
-      if (pd.P > 1 && g < nb) {  // fused pack: c' into the send run of every peer that reads the row
-        const uint32_t pm = pmask[L];
-        const int64_t sb = (b0 + g) * pd.P;
-        for (int q = 0; q < pd.P; ++q) {
-          const bool has = (pm >> q) & 1u;
-          const unsigned long long bal = __ballot(has);
-          if (bal == 0ull) continue;
-          const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-          if (has) pd.sbuf[pd.soff[q] + sbase[sb + q] + k] = cn;
-        }
-      }
-    }
+  for (int64_t gi = g_lo + (int64_t)blockIdx.x * NW + wv; gi < g_hi; gi += nw) epi_group<C, WALK>(a, pd, gi, tdc, win, ep_part);
+}
+
+// Phase ph of k_spmv_hot for iteration i + 1 with epilogue chunk ph + 1 of iteration i beside it, in
+// one launch (PR_BOPT_EPI_OVERLAP; P = 1, compact codes).  The epilogue is bound by HBM streaming
+// (LDS-DMA of the partial runs) and k_spmv_hot by the address unit's divergent gathers, so the
+// last kEpiWaves waves of every workgroup run the epilogue groups [g_lo, g_hi) -- the rows of the
+// class regions hot phase ph + 1 will read -- while the others run the phase's wave units, and
+// then join them (units come from the workgroup's LDS counter, so no wave idles while units are
+// left).  The hot set leaves room for the epilogue waves' windows after the staging windows
+// (pr_build.hip caps the hot slots).  The epilogue reads the partial buffer the previous hot pass
+// wrote (ea.partial) while this phase writes the other one (partial), and it touches only the rows
+// (r, c') of its chunk, which no hot phase of this launch reads.  Group partials go to
+// ep_part[gi] (epi_group), so the sums are bitwise those of the one-pass epilogue.
+template <int CODE, int C, bool WALK>
+__global__ __launch_bounds__(kHotThreads) void k_spmv_hot_epi(
+    const Unit *__restrict__ units, const int64_t *__restrict__ ucum, HotGeom hg, CodeSrc cd,
+    const double *__restrict__ cin, double *__restrict__ partial, const int64_t *__restrict__ poff,
+    double *__restrict__ piece_part, const int32_t *__restrict__ hpos, int ph, EpiArgs ea,
+    const double *__restrict__ ecin, SlotPos sp, double n_vertices, int64_t g_lo, int64_t g_hi,
+    double2 *__restrict__ ep_part, PackDst pd) {
+  static_assert(CODE == kCodeC20 || CODE == kCodeC24, "one part, compact codes");
+  extern __shared__ double hot[];
+  ClassSrc cs;
+  cs.zb = (uint32_t)hg.slots() * 8u;
+  cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
+  cs.tbl = nullptr;
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  double *stage = hot + hg.stage_off() + wv * kStageSlots;
+  const int team = (int)(blockIdx.x / kXcds), nteams = (int)(gridDim.x / kXcds);
+  const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
+  const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;  // region index q_load + 1 + k -> x*Q_pad + q_load + k
+  cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0, (uint32_t)((hg.Q_pad - hg.q_load) * 8),
+                                             0x00020000);
+  stage_hot_set<false>(hg, x, hpos, nullptr, cin, hot, nullptr);
+  __syncthreads();
+  constexpr int kFirstEpi = kHotThreads / kWave - kEpiWaves;
+  if (wv >= kFirstEpi) {
+    const int e = wv - kFirstEpi;
+    double *win = hot + hg.lds_bytes() / sizeof(double) + e * (kEpiWin + 2);
+    if (lane_id() == 0) win[kEpiWin] = 0.0;  // the zero slot
+    const double tdc = dc_from_slots(ecin, sp) / n_vertices;
+    const int64_t nw = (int64_t)gridDim.x * kEpiWaves;
+    for (int64_t gi = g_lo + (int64_t)blockIdx.x * kEpiWaves + e; gi < g_hi; gi += nw)
+      epi_group<C, WALK>(ea, pd, gi, tdc, win, ep_part);
   }
-  double2 *red2 = reinterpret_cast<double2 *>(epi_lds + NW * (W + 2));
-  const double2 part = block_sum2<NT>(make_double2(dcp, l1p), red2);
-  if (threadIdx.x == 0) ep_part[blockIdx.x] = part;
+  hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
+}
+
+using HotEpiFn = void (*)(const Unit *, const int64_t *, HotGeom, CodeSrc, const double *, double *, const int64_t *,
+                          double *, const int32_t *, int, EpiArgs, const double *, SlotPos, double, int64_t, int64_t,
+                          double2 *, PackDst);
+template <int CODE>
+inline HotEpiFn hot_epi_kernel_code(int C, bool walk) {
+  switch (C) {
+    case 16: return walk ? k_spmv_hot_epi<CODE, 16, true> : k_spmv_hot_epi<CODE, 16, false>;
+    case 32: return walk ? k_spmv_hot_epi<CODE, 32, true> : k_spmv_hot_epi<CODE, 32, false>;
+    case 64: return walk ? k_spmv_hot_epi<CODE, 64, true> : k_spmv_hot_epi<CODE, 64, false>;
+    default: return nullptr;
+  }
+}
+inline HotEpiFn hot_epi_kernel(int code, int C, bool walk) {
+  if (code == kCodeC20) return hot_epi_kernel_code<kCodeC20>(C, walk);
+  if (code == kCodeC24) return hot_epi_kernel_code<kCodeC24>(C, walk);
+  return nullptr;
 }
 
 // Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks.
