@@ -753,7 +753,7 @@ def test_epilogue_overlap_bitwise(hip, oracle_c, classes, walk):
     assert np.array_equal(r0, r1) and np.array_equal(s0, s1) and np.array_equal(r1, s1)
     for (a, sa), (b, sb) in zip(h0, h1):
         assert np.array_equal(a, b)
-        assert sa.dc == sb.dc and sa.l1 == sb.l1
+        assert sa.dangling_sum == sb.dangling_sum and sa.l1_delta == sb.l1_delta
     assert st1["spmv_launches"] == iters and st1["spmv_ms_mean"] > 0 and st1["iter_ms_mean"] > 0
     assert st0["last_dc"] == st1["last_dc"] and st0["last_l1"] == st1["last_l1"]
     for it in range(iters):
