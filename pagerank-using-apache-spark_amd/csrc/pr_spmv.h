@@ -646,23 +646,35 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
 // slots 1..nh, the 0.0 slots and the workgroup's unit counter (all 1024 threads; the caller's
 // barrier follows): every position load, then every gather in flight before the first LDS write --
 // a rolled loop pays two dependent memory latencies per element, 18 times per phase (-2.7 % at s26).
-template <bool PIECE>
+// CONTIG (one part, compact codes): the hot set is the first q_load positions of class x's region
+// (pr_build.hip k_hot_tables), so it is read straight from there, one coalesced load per element
+// and no dependent position load.
+template <bool PIECE, bool CONTIG = false>
 __device__ __forceinline__ void stage_hot_set(const HotGeom &hg, int x, const int32_t *__restrict__ hpos,
                                               const int32_t *__restrict__ ptab, const double *__restrict__ cin,
                                               double *hot, uint32_t *tblw) {
   const int nh = hg.P * hg.Kp;
   const int32_t *hp = hpos + (int64_t)x * nh;
+  const double *reg = cin + (int64_t)x * hg.Q_pad;
   constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18429 slots)
   for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
     int32_t pos[kSB];
     double val[kSB];
+    if constexpr (CONTIG) {
 #pragma unroll
-    for (int j = 0; j < kSB; ++j) {
-      const int i = b0 + (int)threadIdx.x + j * kHotThreads;
-      pos[j] = i < nh ? hp[i] : -1;
+      for (int j = 0; j < kSB; ++j) {
+        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+        val[j] = i < hg.q_load ? reg[i] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) {
+        const int i = b0 + (int)threadIdx.x + j * kHotThreads;
+        pos[j] = i < nh ? hp[i] : -1;
+      }
+#pragma unroll
+      for (int j = 0; j < kSB; ++j) val[j] = pos[j] >= 0 ? cin[pos[j]] : 0.0;
     }
-#pragma unroll
-    for (int j = 0; j < kSB; ++j) val[j] = pos[j] >= 0 ? cin[pos[j]] : 0.0;
 #pragma unroll
     for (int j = 0; j < kSB; ++j) {
       const int i = b0 + (int)threadIdx.x + j * kHotThreads;
@@ -713,7 +725,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                  (uint32_t)((hg.Q_pad - hg.q_load) * 8), 0x00020000);
     }
     if (ph > ph0) __syncthreads();  // every wave is done with the previous class's hot set
-    stage_hot_set<kPiece>(hg, x, hpos, ptab, cin, hot, tblw);
+    stage_hot_set<kPiece, CODE == kCodeC20 || CODE == kCodeC24>(hg, x, hpos, ptab, cin, hot, tblw);
     __syncthreads();
     hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
   }
@@ -1055,7 +1067,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot_epi(
   const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;  // region index q_load + 1 + k -> x*Q_pad + q_load + k
   cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0, (uint32_t)((hg.Q_pad - hg.q_load) * 8),
                                              0x00020000);
-  stage_hot_set<false>(hg, x, hpos, nullptr, cin, hot, nullptr);
+  stage_hot_set<false, true>(hg, x, hpos, nullptr, cin, hot, nullptr);
   __syncthreads();
   constexpr int kFirstEpi = kHotThreads / kWave - kEpiWaves;
   if (wv >= kFirstEpi) {
