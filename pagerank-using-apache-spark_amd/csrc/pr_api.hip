@@ -122,6 +122,10 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_OVERLAP: 0 (after the pass) or 1 (beside the next hot phases)");
         o->epi_overlap = v == 1;
         break;
+      case PR_BOPT_EPI_CUS:
+        if (v < 1 || v > 16) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_CUS: 1..16 epilogue CUs per XCD");
+        o->epi_cus = (int)v;
+        break;
       case PR_BOPT_XCHG_SDMA:
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_XCHG_SDMA: 0 (device copies) or 1 (copy engines)");
         o->xchg_sdma = v == 1;

@@ -817,17 +817,9 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                                                      : kCodeU32;
       if (code_is_piece(g->code)) slots = ps;
     }
-    // epilogue overlap (k_spmv_hot_epi): one part, compact codes, 16..64 classes; the hot set
-    // leaves LDS room for the epilogue waves' windows
+    // epilogue overlap (k_spmv_hot_epi): one part, compact codes, 16..64 classes
     const bool overlap = g->opts.epi_overlap && P == 1 && C >= 2 * kXcds && C <= kWave &&
                          (g->code == kCodeC20 || g->code == kCodeC24);
-    if (overlap) {
-      HotGeom t{};
-      t.P = 1;
-      for (t.Kp = slots; t.Kp > 0 && hot_epi_lds(t) > (size_t)kHotLdsBytes; --t.Kp) {
-      }
-      slots = t.Kp;
-    }
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
@@ -987,6 +979,10 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     if (g->n_echunks < 2 || g->ep_chunk_groups * g->n_echunks != ep_parts)
       return fail(PR_ERR_STATE, "epilogue chunks do not tile the groups");
     g->ep_blocks0 = (int)grid_for(g->ep_chunk_groups, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
+    if (g->hot_grid / kXcds - g->opts.epi_cus < 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_CUS leaves no hot CU");
+    PR_TRY(g->ectr.alloc(sizeof(unsigned) * (size_t)g->n_echunks));
+    PR_HIP(hipMemsetAsync(g->ectr.p, 0, sizeof(unsigned) * (size_t)g->n_echunks, s));
+    PR_HIP(hipStreamSynchronize(s));
   }
   // finalize input: fused-unit partials (C = 1) or the split epilogue's group partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + ep_parts + 1)));

@@ -44,6 +44,7 @@ struct pr_build_opts {
   bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
   bool xchg_sdma = false;  // group path: runs move on the copy engines (hipMemcpyDeviceToDeviceNoCU)
   bool epi_overlap = false;  // P = 1 split layout: epilogue chunks beside the next iteration's hot phases
+  int epi_cus = pr::kEpiCusDefault;  // with epi_overlap: epilogue CUs per XCD
 };
 
 struct pr_graph {
@@ -117,6 +118,7 @@ struct pr_graph {
   int pend_in = 0, pend_out = 0, pend_pbuf = 0;
   int n_echunks = 0, ep_blocks0 = 0;
   int64_t ep_chunk_groups = 0;
+  pr::DevBuf ectr;  // per chunk: the next group k_spmv_hot_epi hands out (zeroed by k_finalize)
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;
   pr::DevBuf fin_part, fin_counter;

@@ -47,8 +47,9 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
     double *__restrict__ r, const uint32_t *__restrict__ rowinfo, const double *__restrict__ cin,
     double *__restrict__ cout, SlotPos sp, double n_vertices, double teleport,
     double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
-    double *__restrict__ slot_out, PackSlots ps) {
+    double *__restrict__ slot_out, PackSlots ps, unsigned *__restrict__ zero, int n_zero) {
   __shared__ double red[kThreads / kWave];
+  if (blockIdx.x == 0 && (int)threadIdx.x < n_zero) zero[threadIdx.x] = 0u;  // k_spmv_hot_epi's group counters
   __shared__ int is_last;
   const int t = threadIdx.x, lane = lane_id();
   double dcp = 0.0, l1p = 0.0;
@@ -145,7 +146,7 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
                      parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[in_buf].as<double>(), cout, g->slots, (double)g->V,
                      g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
-                     cout + g->S_pad - 2, ps);
+                     cout + g->S_pad - 2, ps, g->ectr.as<unsigned>(), g->epi_overlap ? g->n_echunks : 0);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
@@ -383,9 +384,10 @@ int iter_compute_overlap(pr_graph *g) {
       const int64_t g0 = (int64_t)(c + 1) * g->ep_chunk_groups;
       hipLaunchKernelGGL(fused, dim3((unsigned)g->hot_grid), dim3(kHotThreads), hot_epi_lds(g->hot), s,
                          g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
-                         partial_buf(g), g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), c, ea,
-                         g->cbuf[g->pend_in].as<double>(), g->slots, (double)g->V, g0, g0 + g->ep_chunk_groups,
-                         g->unit_part.as<double2>() + g->n_units, PackDst{});
+                         partial_buf(g), g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), c,
+                         g->opts.epi_cus, ea, g->cbuf[g->pend_in].as<double>(), g->slots, (double)g->V, g0,
+                         g0 + g->ep_chunk_groups, g->ectr.as<unsigned>() + c, g->unit_part.as<double2>() + g->n_units,
+                         PackDst{});
       PR_HIP(hipGetLastError());
       if (c + 1 == g->n_echunks - 1)  // the last chunk of i - 1 is out: its finalize (dc of i)
         PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + epi_groups(g), g->pend_in,

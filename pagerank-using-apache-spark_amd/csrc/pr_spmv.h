@@ -1037,54 +1037,69 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
 }
 
 // Phase ph of k_spmv_hot for iteration i + 1 with epilogue chunk ph + 1 of iteration i beside it, in
-// one launch (PR_BOPT_EPI_OVERLAP; P = 1, compact codes).  The epilogue is bound by HBM streaming
-// (LDS-DMA of the partial runs) and k_spmv_hot by the address unit's divergent gathers, so the
-// last kEpiWaves waves of every workgroup run the epilogue groups [g_lo, g_hi) -- the rows of the
-// class regions hot phase ph + 1 will read -- while the others run the phase's wave units, and
-// then join them (units come from the workgroup's LDS counter, so no wave idles while units are
-// left).  The hot set leaves room for the epilogue waves' windows after the staging windows
-// (pr_build.hip caps the hot slots).  The epilogue reads the partial buffer the previous hot pass
-// wrote (ea.partial) while this phase writes the other one (partial), and it touches only the rows
-// (r, c') of its chunk, which no hot phase of this launch reads.  Group partials go to
-// ep_part[gi] (epi_group), so the sums are bitwise those of the one-pass epilogue.
+// one launch (PR_BOPT_EPI_OVERLAP; P = 1, compact codes).  k_spmv_hot is bound by its CU's vector-
+// memory path (the divergent gathers keep the address unit ~96 % busy) and the epilogue by HBM
+// streaming (LDS-DMA of the partial runs), so the two get DIFFERENT CUs: one 1024-thread workgroup
+// per CU as k_spmv_hot, and on every XCD the last `epi_cus` workgroups (grid slots b / 8 >= 32 -
+// epi_cus) run epilogue groups with 16 waves of 8 KiB windows while the others run the phase's
+// wave units as k_spmv_hot's teams.  (Epilogue waves placed beside the hot waves of the same CU
+// took 2.8x the phase: their loads queue behind the gathers at the CU's address unit,
+// profiles/r04/README.md.)  Groups come from a device counter (ectr, zeroed by k_finalize each
+// iteration), and a hot workgroup that has finished its units reuses its LDS as 16 windows and
+// takes groups too, so whichever side finishes first helps the other's tail.  The epilogue reads
+// the partial buffer the previous hot pass wrote (ea.partial) while this phase writes the other
+// one, and it touches only the rows (r, c') of its chunk, which no hot phase of this launch reads.
+// Group partials go to ep_part[gi] (epi_group): the sums are bitwise those of the one-pass epilogue.
+template <int C, bool WALK>
+__device__ __forceinline__ void epi_groups_dynamic(const EpiArgs &ea, const PackDst &pd, int64_t g_lo, int64_t g_hi,
+                                                   unsigned *ectr, double tdc, double *win, double2 *ep_part) {
+  const int lane = lane_id();
+  if (lane == 0) win[kEpiWin] = 0.0;  // the zero slot
+  while (true) {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(ectr, 1u);
+    const int64_t gi = g_lo + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (gi >= g_hi) break;
+    epi_group<C, WALK>(ea, pd, gi, tdc, win, ep_part);
+  }
+}
+
 template <int CODE, int C, bool WALK>
 __global__ __launch_bounds__(kHotThreads) void k_spmv_hot_epi(
     const Unit *__restrict__ units, const int64_t *__restrict__ ucum, HotGeom hg, CodeSrc cd,
     const double *__restrict__ cin, double *__restrict__ partial, const int64_t *__restrict__ poff,
-    double *__restrict__ piece_part, const int32_t *__restrict__ hpos, int ph, EpiArgs ea,
+    double *__restrict__ piece_part, const int32_t *__restrict__ hpos, int ph, int epi_cus, EpiArgs ea,
     const double *__restrict__ ecin, SlotPos sp, double n_vertices, int64_t g_lo, int64_t g_hi,
-    double2 *__restrict__ ep_part, PackDst pd) {
+    unsigned *__restrict__ ectr, double2 *__restrict__ ep_part, PackDst pd) {
   static_assert(CODE == kCodeC20 || CODE == kCodeC24, "one part, compact codes");
   extern __shared__ double hot[];
+  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
+  const int nteams = (int)(gridDim.x / kXcds) - epi_cus, team = (int)(blockIdx.x / kXcds);
+  double *win = hot + wv * (kEpiWin + 2);  // an epilogue wave's window (after the hot work, for hot teams)
+  const double tdc = dc_from_slots(ecin, sp) / n_vertices;
+  if (team >= nteams) {  // an epilogue CU
+    epi_groups_dynamic<C, WALK>(ea, pd, g_lo, g_hi, ectr, tdc, win, ep_part);
+    return;
+  }
   ClassSrc cs;
   cs.zb = (uint32_t)hg.slots() * 8u;
   cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
   cs.tbl = nullptr;
-  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
   double *stage = hot + hg.stage_off() + wv * kStageSlots;
-  const int team = (int)(blockIdx.x / kXcds), nteams = (int)(gridDim.x / kXcds);
   const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
   const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;  // region index q_load + 1 + k -> x*Q_pad + q_load + k
   cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0, (uint32_t)((hg.Q_pad - hg.q_load) * 8),
                                              0x00020000);
   stage_hot_set<false, true>(hg, x, hpos, nullptr, cin, hot, nullptr);
   __syncthreads();
-  constexpr int kFirstEpi = kHotThreads / kWave - kEpiWaves;
-  if (wv >= kFirstEpi) {
-    const int e = wv - kFirstEpi;
-    double *win = hot + hg.lds_bytes() / sizeof(double) + e * (kEpiWin + 2);
-    if (lane_id() == 0) win[kEpiWin] = 0.0;  // the zero slot
-    const double tdc = dc_from_slots(ecin, sp) / n_vertices;
-    const int64_t nw = (int64_t)gridDim.x * kEpiWaves;
-    for (int64_t gi = g_lo + (int64_t)blockIdx.x * kEpiWaves + e; gi < g_hi; gi += nw)
-      epi_group<C, WALK>(ea, pd, gi, tdc, win, ep_part);
-  }
   hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
+  __syncthreads();  // every wave is done with the hot set: its LDS becomes 16 epilogue windows
+  epi_groups_dynamic<C, WALK>(ea, pd, g_lo, g_hi, ectr, tdc, win, ep_part);
 }
 
 using HotEpiFn = void (*)(const Unit *, const int64_t *, HotGeom, CodeSrc, const double *, double *, const int64_t *,
-                          double *, const int32_t *, int, EpiArgs, const double *, SlotPos, double, int64_t, int64_t,
-                          double2 *, PackDst);
+                          double *, const int32_t *, int, int, EpiArgs, const double *, SlotPos, double, int64_t, int64_t,
+                          unsigned *, double2 *, PackDst);
 template <int CODE>
 inline HotEpiFn hot_epi_kernel_code(int C, bool walk) {
   switch (C) {

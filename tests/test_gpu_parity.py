@@ -716,27 +716,25 @@ def test_compact_codes_widen_then_fall_back(hip, oracle_c, V, bits):
             r32, _ = g.run(4)
         assert np.array_equal(r32, ranks)
 
-@pytest.mark.parametrize("classes,walk", [(16, 1), (32, 1), (64, 1), (64, 0)])
-def test_epilogue_overlap_bitwise(hip, oracle_c, classes, walk):
-    """PR_BOPT_EPI_OVERLAP: the epilogue of iteration i runs in class-region chunks on a second stream
-    beside the hot phases of i + 1, on double-buffered partial slots, with a hot set trimmed to leave
-    LDS for two epilogue waves per CU.  Whether a value comes from LDS or the gather space and which
-    stream runs a chunk do not change any sum: the ranks, dc and L1 of every iteration are bitwise
-    those of the serial pass, through the step API (no host sync between iterations), through pr_run
-    with a per-iteration callback (a join every iteration) and after a reset mid-stream."""
-    rng = np.random.default_rng(classes + walk)
+@pytest.mark.parametrize("classes,walk,cus", [(16, 1, 4), (32, 1, 4), (64, 1, 4), (64, 0, 2), (64, 1, 16)])
+def test_epilogue_overlap_bitwise(hip, oracle_c, classes, walk, cus):
+    """PR_BOPT_EPI_OVERLAP: the epilogue of iteration i runs in class-region chunks on `cus` CUs per XCD
+    while the other CUs run the hot phases of i + 1 (k_spmv_hot_epi), on double-buffered partial slots,
+    groups handed out dynamically.  Which CU or launch runs a group does not change any sum (group
+    partials are written per group): the ranks, dc and L1 of every iteration are bitwise those of the
+    serial pass, through the step API (no host sync between iterations), through pr_run with a
+    per-iteration callback (a join every iteration) and after a reset mid-stream."""
+    rng = np.random.default_rng(classes + walk + cus)
     V = 60000
     src, dst = random_edges(rng, V, 900000, hub_frac=0.02)
     iters = 9
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), iters, keep_history=True)
     out = {}
     for ov in (0, 1):
-        opts = {"classes": classes, "epi_walk": walk, "epi_overlap": ov}
+        opts = {"classes": classes, "epi_walk": walk, "epi_overlap": ov, "epi_cus": cus}
         with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split", options=opts) as g:
             info = g.info()
             assert info["classes"] == classes and info["epilogue"] == (4 if ov else 3)
-            if ov:
-                assert info["hot_slots"] < 18429  # LDS left for the co-resident epilogue waves
             hist = []
             ranks_cb, st = g.run(iters, want_ranks_in_callback=True, callback=lambda it, r, s: hist.append((r, s)))
             g.reset()
