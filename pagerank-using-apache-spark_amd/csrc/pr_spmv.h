@@ -830,9 +830,18 @@ struct EpiArgs {
 // same order whichever wave, workgroup or launch ran the group: every epilogue schedule (one
 // pass, chunks on a second stream, epilogue waves inside k_spmv_hot_epi) is bitwise the same.
 // The body of k_epilogue_grp (below) and of k_spmv_hot_epi's epilogue waves.
-template <int C, bool WALK>
+//
+// NT (k_spmv_hot_epi, PR_EPI_NT): every load and store of the group is non-temporal (LDS-DMA with
+// the nt policy, aux = 2), so the streamed partial runs and row data do not evict the class
+// region the hot phase running beside it gathers from its XCD's L2.
+template <int C, bool WALK, bool NT = false>
 __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, int64_t gi, double tdc, double *win,
                                           double2 *__restrict__ ep_part) {
+  constexpr int kAux = NT ? 2 : 0;
+  auto ld = [](const auto *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+  };
   double dcp = 0.0, l1p = 0.0;
   constexpr int G = kEpiGroup, W = kEpiWin;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
@@ -849,22 +858,22 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     const int64_t L = (b0 + g) * kWave + lane;
     const bool ok = g < nb;
     if constexpr (MW == 4) {
-      const uint4 q = ok ? static_cast<const uint4 *>(a.rmask)[L] : make_uint4(0u, 0u, 0u, 0u);
-      mw[0][g] = q.x, mw[1][g] = q.y, mw[2][g] = q.z, mw[3][g] = q.w;
+      const pr_v4i q = ok ? ld(static_cast<const pr_v4i *>(a.rmask) + L) : pr_v4i{0, 0, 0, 0};
+      mw[0][g] = (uint32_t)q.x, mw[1][g] = (uint32_t)q.y, mw[2][g] = (uint32_t)q.z, mw[3][g] = (uint32_t)q.w;
     } else if constexpr (MW == 2) {
-      const uint2 q = ok ? static_cast<const uint2 *>(a.rmask)[L] : make_uint2(0u, 0u);
-      mw[0][g] = q.x, mw[1][g] = q.y;
+      const uint64_t q = ok ? ld(static_cast<const uint64_t *>(a.rmask) + L) : 0ull;
+      mw[0][g] = (uint32_t)q, mw[1][g] = (uint32_t)(q >> 32);
     } else {
-      mw[0][g] = ok ? static_cast<const uint32_t *>(a.rmask)[L] : 0u;
+      mw[0][g] = ok ? ld(static_cast<const uint32_t *>(a.rmask) + L) : 0u;
     }
-    info[g] = ok ? a.rowinfo[L] : kRowHole;
-    rold[g] = ok ? a.r[L] : 0.0;
+    info[g] = ok ? ld(a.rowinfo + L) : kRowHole;
+    rold[g] = ok ? ld(a.r + L) : 0.0;
     S[g] = 0.0;
   }
   // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
   // per class with v_readlane
-  const int cs = lane < C ? a.cbase[b0 * C + lane] : 0;
-  const int ce = lane < C ? a.cbase[(b0 + nb) * C + lane] : 0;
+  const int cs = lane < C ? ld(a.cbase + b0 * C + lane) : 0;
+  const int ce = lane < C ? ld(a.cbase + (b0 + nb) * C + lane) : 0;
   if constexpr (C <= kWave) {
     // lane y: class y's run start rounded down to 16 bytes (sa), its staged length n2 (0: no
     // slots in this group) and its window position, the exclusive prefix of n2 over the
@@ -887,13 +896,13 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
           const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
           double *dst = win + __builtin_amdgcn_readlane(pre, y);
           for (int o = 0; o < n; o += 2 * kWave)
-            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, kAux);
         }
         const int Tb = __builtin_amdgcn_readlane(incl, C - 1);  // staged slots (even)
         const int nl = (__builtin_amdgcn_readlane(sincl, C - 1) + 7) >> 3;  // 16-byte lanes of positions
         const double *esrc = reinterpret_cast<const double *>(a.epos + eo);
         for (int o = 0; o < nl; o += kWave)
-          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
+          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, kAux);
         __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
         const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
         int acc = 0;  // index of block g's first position
@@ -921,7 +930,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
         double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
         for (int o = 0; o < n; o += 2 * kWave)
-          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, kAux);
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
       for (int y = x0; y < x1; ++y) {
@@ -953,7 +962,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         if (xe > x && fill + n2 > W) break;
         const double *src = a.partial + sa;
         for (int o = 0; o < n2; o += 2 * kWave)
-          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
+          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, kAux);
         fill += n2;
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
@@ -986,11 +995,13 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     const double rn = affine(Sv, tdc, a.teleport, a.damping);
     double cn = 0.0;
     if (!(info[g] & kRowHole)) {
-      a.r[L] = rn;
+      if constexpr (NT) __builtin_nontemporal_store(rn, a.r + L);
+      else a.r[L] = rn;
       const uint32_t d = info[g] & kRowDegMask;
       if (d > 0) {
         cn = __ddiv_rn(rn, (double)d);
-        a.cout[L] = cn;
+        if constexpr (NT) __builtin_nontemporal_store(cn, a.cout + L);
+        else a.cout[L] = cn;
       } else if (info[g] & kRowSink) {
         dcp = __dadd_rn(dcp, rn);
       }
@@ -1050,17 +1061,21 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
 // the partial buffer the previous hot pass wrote (ea.partial) while this phase writes the other
 // one, and it touches only the rows (r, c') of its chunk, which no hot phase of this launch reads.
 // Group partials go to ep_part[gi] (epi_group): the sums are bitwise those of the one-pass epilogue.
+#ifndef PR_EPI_NT
+#define PR_EPI_NT 1
+#endif
 template <int C, bool WALK>
 __device__ __forceinline__ void epi_groups_dynamic(const EpiArgs &ea, const PackDst &pd, int64_t g_lo, int64_t g_hi,
                                                    unsigned *ectr, double tdc, double *win, double2 *ep_part) {
   const int lane = lane_id();
   if (lane == 0) win[kEpiWin] = 0.0;  // the zero slot
+  unsigned t = 0;
+  if (lane == 0) t = atomicAdd(ectr, 1u);
   while (true) {
-    unsigned t = 0;
-    if (lane == 0) t = atomicAdd(ectr, 1u);
     const int64_t gi = g_lo + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
     if (gi >= g_hi) break;
-    epi_group<C, WALK>(ea, pd, gi, tdc, win, ep_part);
+    if (lane == 0) t = atomicAdd(ectr, 1u);  // the next group's ticket, in flight during this group
+    epi_group<C, WALK, PR_EPI_NT != 0>(ea, pd, gi, tdc, win, ep_part);
   }
 }
 
