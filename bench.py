@@ -552,7 +552,6 @@ def main() -> int:
                 "layout": ["fused", "split"][info.get("layout", 0)],
                 "hot_cover": round(info.get("hot_cover_ppm", 0) / 1e6, 4),
                 "code_bits": info.get("code_bits"),
-                "epilogue_overlap": info.get("epilogue") == 4,
                 # --share-device: a correctness rehearsal (ranks share GPUs, RCCL over loopback sockets)
                 "shared_device_rehearsal": bool(a.share_device and world > 1),
             },

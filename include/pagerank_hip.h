@@ -70,7 +70,7 @@ extern "C" {
 #define PR_INFO_XCHG_RECV 15   /* doubles this part receives per iteration (P > 1)        */
 #define PR_INFO_PARTIAL_SLOTS 16 /* (row, column class) segment sums of the split layout     */
 #define PR_INFO_HOT_SLOTS 17   /* LDS hot-set contributions per class (split layout)        */
-#define PR_INFO_EPILOGUE 18    /* 0 fused units, 3 grouped (split), 4 grouped in chunks beside the next hot phases */
+#define PR_INFO_EPILOGUE 18    /* 0 fused units, 3 grouped (split)                           */
 #define PR_INFO_GATHER_EST 19  /* bytes of the part's expected gather space (class policy)   */
 #define PR_INFO_WALK_GROUPS 20 /* epilogue groups (8 x 64 rows) that walk their rows' own slots */
 #define PR_INFO_LAYOUT 21      /* 0 fused, 1 split (column classes + partial slots)          */
@@ -139,11 +139,6 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_XCHG_SDMA 10  /* group path (pr_group_*, P > 1 per-peer runs): 0 (default) the runs move by
                                  device copies (ROCclr blit kernels on the CUs), 1 by the copy engines
                                  (hipMemcpyDeviceToDeviceNoCU), which leave k_spmv_hot every CU */
-#define PR_BOPT_EPI_OVERLAP 11 /* split layout, P = 1, compact codes, 16..64 classes: 1 = the epilogue of
-                                 iteration i runs in class-region chunks on PR_BOPT_EPI_CUS CUs per XCD while
-                                 the others run the hot phases of i + 1 (chunk c ends before phase c starts;
-                                 double-buffered partial slots), 0 = after the pass (default); same values */
-#define PR_BOPT_EPI_CUS 12    /* with PR_BOPT_EPI_OVERLAP: epilogue CUs per XCD, 1..16 (default 4) */
 int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
                        const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
                        int32_t n_options, pr_graph **out);

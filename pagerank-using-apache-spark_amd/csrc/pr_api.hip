@@ -43,7 +43,7 @@ void DevBuf::reset() {
 
 size_t pr_graph::device_bytes() const {
   size_t b = canon_rowptr.bytes + canon_col.bytes + canon_deg.bytes + canon_vflags.bytes;
-  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + partial2.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
+  b += rowptr.bytes + col.bytes + colp.bytes + rowinfo.bytes + colh.bytes + hunits.bytes + partial.bytes + poff.bytes + rmask.bytes + cbase.bytes + seg_slot.bytes + seg_p0.bytes + r.bytes + cbuf[0].bytes + cbuf[1].bytes + eoff.bytes + epos.bytes;
   b += units.bytes + unit_part.bytes + lr_row.bytes + lr_p0.bytes + piece_part.bytes;
   b += fin_part.bytes + fin_counter.bytes + reset_part.bytes + x_send.bytes + x_sbuf.bytes + hpos.bytes + cside.bytes;
   return b;
@@ -117,14 +117,6 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
       case PR_BOPT_PACK_FUSED:
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_PACK_FUSED: 0 (pack kernel) or 1 (in the epilogue)");
         o->pack_fused = v == 1;
-        break;
-      case PR_BOPT_EPI_OVERLAP:
-        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_OVERLAP: 0 (after the pass) or 1 (beside the next hot phases)");
-        o->epi_overlap = v == 1;
-        break;
-      case PR_BOPT_EPI_CUS:
-        if (v < 1 || v > 16) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_CUS: 1..16 epilogue CUs per XCD");
-        o->epi_cus = (int)v;
         break;
       case PR_BOPT_XCHG_SDMA:
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_XCHG_SDMA: 0 (device copies) or 1 (copy engines)");
@@ -229,7 +221,7 @@ int pr_graph_info(const pr_graph *g, int64_t *info, int32_t n_info) {
                                     (int64_t)g->device_bytes(), g->C,
                                     xchg_volume(g, true), xchg_volume(g, false), g->n_slots,
                                     g->C > 1 ? (int64_t)g->hot.P * g->hot.Kp : 0,
-                                    g->C == 1 ? 0 : (g->epi_overlap ? 4 : 3), g->gather_est, g->n_walk_groups, g->layout,
+                                    g->C == 1 ? 0 : 3, g->gather_est, g->n_walk_groups, g->layout,
                                     g->hot_cover_ppm, g->C > 1 ? (g->code == pr::kCodeC20 || g->code == pr::kCodeC20P ? 20 : g->code == pr::kCodeC24 || g->code == pr::kCodeC24P ? 24 : 32) : 0};
   for (int32_t i = 0; i < n_info && i < PR_INFO_COUNT; ++i) info[i] = v[i];
   return PR_OK;
@@ -279,7 +271,6 @@ int pr_get_ranks(pr_graph *g, double *ranks_out) {
   if (!g || !ranks_out) return fail(PR_ERR_INVALID, "NULL argument");
   if (!g->ready) return fail(PR_ERR_STATE, "pr_get_ranks before pr_reset");
   DeviceGuard dg(g->device);
-  PR_TRY(pr::join_exchange(g));  // an overlapped epilogue may still be writing r
   std::vector<double> loc((size_t)g->n_rows);
   if (g->n_rows > 0)
     PR_HIP(hipMemcpyAsync(loc.data(), g->r.p, sizeof(double) * g->n_rows, hipMemcpyDeviceToHost, g->stream));

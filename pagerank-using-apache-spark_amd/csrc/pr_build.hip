@@ -817,9 +817,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
                                                      : kCodeU32;
       if (code_is_piece(g->code)) slots = ps;
     }
-    // epilogue overlap (k_spmv_hot_epi): one part, compact codes, 16..64 classes
-    const bool overlap = g->opts.epi_overlap && P == 1 && C >= 2 * kXcds && C <= kWave &&
-                         (g->code == kCodeC20 || g->code == kCodeC24);
     HotGeom hg{};
     hg.C = C;
     hg.P = P;
@@ -871,10 +868,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     }
     // + 2 slots: the grouped epilogue stages class runs in 16-byte pairs (one slot past the end)
     PR_TRY(g->partial.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
-    if (overlap) {  // the hot kernel of iteration i + 1 fills the other buffer
-      PR_TRY(g->partial2.alloc(sizeof(double) * (size_t)(poff[C] + 2)));
-      g->epi_overlap = true;
-    }
     g->n_slots = poff[C];
     PR_HIP(hipMemcpyAsync(g->hucum.p, sp.ucum.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
     PR_HIP(hipMemcpyAsync(g->poff.p, poff.data(), sizeof(int64_t) * (kMaxClasses + 1), hipMemcpyHostToDevice, s));
@@ -971,19 +964,6 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
   }
   // the split epilogue writes one {dangling, L1} partial per group (pr_spmv.h epi_group)
   const int64_t ep_parts = C > 1 ? (g->nblk + kEpiGroup - 1) / kEpiGroup : 0;
-  if (g->epi_overlap) {
-    // chunk c = the rows of class regions [8c, 8c + 8): Q_pad / 64 groups of 8 blocks (Q_pad is a
-    // multiple of 64, so chunks start on group boundaries)
-    g->n_echunks = n_hot_phases(g);
-    g->ep_chunk_groups = g->Q_pad / kWave;
-    if (g->n_echunks < 2 || g->ep_chunk_groups * g->n_echunks != ep_parts)
-      return fail(PR_ERR_STATE, "epilogue chunks do not tile the groups");
-    g->ep_blocks0 = (int)grid_for(g->ep_chunk_groups, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
-    if (g->hot_grid / kXcds - g->opts.epi_cus < 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_CUS leaves no hot CU");
-    PR_TRY(g->ectr.alloc(sizeof(unsigned) * (size_t)g->n_echunks));
-    PR_HIP(hipMemsetAsync(g->ectr.p, 0, sizeof(unsigned) * (size_t)g->n_echunks, s));
-    PR_HIP(hipStreamSynchronize(s));
-  }
   // finalize input: fused-unit partials (C = 1) or the split epilogue's group partials (C > 1)
   PR_TRY(g->unit_part.alloc(sizeof(double) * 2 * ((size_t)g->n_units + ep_parts + 1)));
   PR_TRY(g->reset_part.alloc(sizeof(double) * 2 * g->reset_blocks));

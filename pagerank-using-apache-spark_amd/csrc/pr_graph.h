@@ -43,8 +43,6 @@ struct pr_build_opts {
   int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
   bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
   bool xchg_sdma = false;  // group path: runs move on the copy engines (hipMemcpyDeviceToDeviceNoCU)
-  bool epi_overlap = false;  // P = 1 split layout: epilogue chunks beside the next iteration's hot phases
-  int epi_cus = pr::kEpiCusDefault;  // with epi_overlap: epilogue CUs per XCD
 };
 
 struct pr_graph {
@@ -103,22 +101,6 @@ struct pr_graph {
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   int64_t hot_cover_ppm = 0;  // in-links whose source is in a class's hot set (layout policy input)
   pr::DevBuf cbuf[2];
-  // Epilogue overlap (PR_BOPT_EPI_OVERLAP, pr_iter.hip iter_compute_overlap): the epilogue of
-  // iteration i is cut into n_echunks chunks of ep_chunk_groups groups -- chunk c = the rows of the
-  // class regions hot phase c reads.  Chunk 0 runs alone after the hot pass (ep_blocks0
-  // workgroups); chunk c >= 1 runs inside the launch of hot phase c - 1 of iteration i + 1
-  // (k_spmv_hot_epi), and the finalize of i before phase n_echunks - 1.  The hot pass of i + 1
-  // writes the other partial buffer (partial / partial2, pbuf) while the epilogue of i reads this
-  // one.  epi_pending: chunks >= 1 and the finalize of the last iteration (pend_*) are not launched
-  // yet; join_exchange launches them before anything reads ranks, slots or contributions.
-  bool epi_overlap = false;
-  int pbuf = 0;
-  pr::DevBuf partial2;
-  bool epi_pending = false;
-  int pend_in = 0, pend_out = 0, pend_pbuf = 0;
-  int n_echunks = 0, ep_blocks0 = 0;
-  int64_t ep_chunk_groups = 0;
-  pr::DevBuf ectr;  // per chunk: the next group k_spmv_hot_epi hands out (zeroed by k_finalize)
   pr::DevBuf units, unit_part;
   pr::DevBuf lr_row, lr_p0, piece_part;
   pr::DevBuf fin_part, fin_counter;
@@ -195,7 +177,7 @@ int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (afte
 int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);
-int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange (and epilogue)
+int join_exchange(pr_graph *g);  // g's stream waits for a pending overlapped exchange
 // x_chunked from the build option (1: the overlapped exchange; 0: whole runs, the next iteration
 // waits for all of them).  Off by default: the transfers are kernels (RCCL, blit copies) that
 // compete with k_spmv_hot for CUs -- k_spmv_hot takes a CU's whole LDS, so the two cannot share
@@ -217,7 +199,6 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a = nullptr, hipEvent_t ev_b = 
 double *send_runs(const pr_graph *g, int buf);  // the packed send runs paired with gather buffer buf
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
-double *partial_buf(const pr_graph *g);  // the partial slots the next hot pass writes (pbuf)
 hipEvent_t next_event(pr_graph *g);  // the next timing event of g's pool (nullptr: creation failed)
 int time_mark(pr_graph *g, hipStream_t s, int *index);  // records one on s; *index into ev_pool
 }  // namespace pr

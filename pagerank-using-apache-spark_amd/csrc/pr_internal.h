@@ -228,14 +228,6 @@ struct HotGeom {
   }
 };
 
-// k_spmv_hot_epi (PR_BOPT_EPI_OVERLAP): epilogue CUs per XCD by default (PR_BOPT_EPI_CUS), and its
-// dynamic LDS: the hot kernel's, or 16 epilogue windows (kEpiWin + 2 slots each), the larger
-constexpr int kEpiCusDefault = 4;
-inline size_t hot_epi_lds(const HotGeom &hg) {
-  const size_t w = sizeof(double) * (kHotThreads / 64) * (kEpiWin + 2);
-  return hg.lds_bytes() > w ? hg.lds_bytes() : w;
-}
-
 // Host plan over a part's row_ptr: units, their source offsets in the unpadded column array,
 // long rows (split into pieces) and the padded column length.
 struct UnitPlan {

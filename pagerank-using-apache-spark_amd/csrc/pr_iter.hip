@@ -47,9 +47,8 @@ __global__ __launch_bounds__(kThreads) void k_finalize(
     double *__restrict__ r, const uint32_t *__restrict__ rowinfo, const double *__restrict__ cin,
     double *__restrict__ cout, SlotPos sp, double n_vertices, double teleport,
     double damping, double *__restrict__ fin_part, unsigned *__restrict__ counter,
-    double *__restrict__ slot_out, PackSlots ps, unsigned *__restrict__ zero, int n_zero) {
+    double *__restrict__ slot_out, PackSlots ps) {
   __shared__ double red[kThreads / kWave];
-  if (blockIdx.x == 0 && (int)threadIdx.x < n_zero) zero[threadIdx.x] = 0u;  // k_spmv_hot_epi's group counters
   __shared__ int is_last;
   const int t = threadIdx.x, lane = lane_id();
   double dcp = 0.0, l1p = 0.0;
@@ -146,14 +145,12 @@ int launch_finalize(pr_graph *g, int64_t n_long, const double2 *parts, int64_t n
                      parts, n_parts, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
                      g->cbuf[in_buf].as<double>(), cout, g->slots, (double)g->V,
                      g->teleport, g->damping, g->fin_part.as<double>(), g->fin_counter.as<unsigned>(),
-                     cout + g->S_pad - 2, ps, g->ectr.as<unsigned>(), g->epi_overlap ? g->n_echunks : 0);
+                     cout + g->S_pad - 2, ps);
   PR_HIP(hipGetLastError());
   return PR_OK;
 }
 
 }  // namespace
-
-double *partial_buf(const pr_graph *g) { return (g->pbuf ? g->partial2 : g->partial).as<double>(); }
 
 hipEvent_t next_event(pr_graph *g) {
   if (g->ev_next >= g->ev_pool.size()) {
@@ -180,11 +177,6 @@ int prepare_hot_kernel() {
         PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
-  for (int code : {kCodeC20, kCodeC24})
-    for (int c : {16, 32, 64})
-      for (bool walk : {false, true})
-        PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(hot_epi_kernel(code, c, walk)),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
                         reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>),
                         reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>),
@@ -262,7 +254,7 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
                                      : k_spmv_hot<kCodeU32>;
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
-                     (uint32_t)(sizeof(double) * g->gsize), partial_buf(g), g->poff.as<int64_t>(),
+                     (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),
                      g->piece_part.as<double>(), g->hpos.as<int32_t>(), g->ptab.as<int32_t>(), ph0, ph1);
   PR_HIP(hipGetLastError());
   return PR_OK;
@@ -270,10 +262,7 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
 
 void set_exchange_chunking(pr_graph *g) { g->x_chunked = g->opts.xchg_chunks && g->n_xc > 1; }
 
-int flush_epilogue(pr_graph *g);
-
 int join_exchange(pr_graph *g) {
-  PR_TRY(flush_epilogue(g));  // the overlapped epilogue's deferred chunks and finalize
   if (!g->x_pending) return PR_OK;
   PR_HIP(hipStreamWaitEvent(g->stream, g->x_ev.back(), 0));  // chunks are recorded in order
   g->x_pending = false;
@@ -293,7 +282,6 @@ int iter_reset(pr_graph *g, const double *init_host) {
     PR_HIP(hipStreamSynchronize(s));
   }
   g->cur = 0;
-  g->pbuf = 0;
   g->x_packed = -1;
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
@@ -316,109 +304,11 @@ int iter_reset(pr_graph *g, const double *init_host) {
   return PR_OK;
 }
 
-// The epilogue overlapped with the next iteration's hot phases (PR_BOPT_EPI_OVERLAP; P = 1, split
-// layout, compact codes).  One stream; iteration i launches
-//   phase 0 of i + epilogue chunk 1 of i - 1    (k_spmv_hot_epi)
-//   ...
-//   phase n-2 of i + epilogue chunk n-1 of i - 1
-//   k_finalize of i - 1                          (dc for the epilogue of i)
-//   phase n-1 of i                               (k_spmv_hot)
-//   k_seg_reduce of i
-//   epilogue chunk 0 of i                        (k_epilogue_grp: phase 0 of i + 1 reads its rows)
-// and leaves chunks 1.. and the finalize of i pending.  Hot phase c reads only the contributions of
-// class regions 8c .. 8c + 7 = epilogue chunk c's rows, written before it in stream order; the hot
-// phases of i write one partial buffer while the epilogue chunks of i - 1 read the other (pbuf);
-// an epilogue chunk writes r and c' of its own rows only.  join_exchange launches what is pending.
-// Timing: one interval per iteration, its first launch to its chunk 0 (the flush of the last
-// iteration's remaining chunks extends the last interval), so the intervals tile the run.
 namespace {
-int launch_epi_range(pr_graph *g, int64_t g0, int64_t g1, int pb, int in, int out) {
-  const int64_t gpc = g->ep_chunk_groups;
-  const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
-  const unsigned blocks = (unsigned)((int64_t)g->ep_blocks0 * ((g1 - g0 + gpc - 1) / gpc));
-  const double *part = (pb ? g->partial2 : g->partial).as<double>();
-  hipLaunchKernelGGL(epi, dim3(blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), g->stream,
-                     g->nblk, g0, g1, part, g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
-                     g->r.as<double>(), g->cbuf[out].as<double>() + g->own_off, g->cbuf[in].as<double>(), g->slots,
-                     (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
-                     g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(),
-                     PackDst{});
-  PR_HIP(hipGetLastError());
-  return PR_OK;
-}
 int64_t epi_groups(const pr_graph *g) { return (g->nblk + kEpiGroup - 1) / kEpiGroup; }
 }  // namespace
 
-int flush_epilogue(pr_graph *g) {
-  if (!g->epi_pending) return PR_OK;
-  g->epi_pending = false;
-  PR_TRY(launch_epi_range(g, g->ep_chunk_groups, epi_groups(g), g->pend_pbuf, g->pend_in, g->pend_out));
-  PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + epi_groups(g), g->pend_in,
-                         g->pend_out, g->stream));
-  if (g->timing && !g->spmv_ev.empty()) {  // the deferred chunks belong to the last timed iteration
-    int e = -1;
-    PR_TRY(time_mark(g, g->stream, &e));
-    g->spmv_ev.back().second = e;
-    if (!g->iter_ev.empty()) g->iter_ev.back().second = e;
-  }
-  return PR_OK;
-}
-
-int iter_compute_overlap(pr_graph *g) {
-  hipStream_t s = g->stream;
-  const int in = g->cur, out = g->cur ^ 1;
-  const int nph = n_hot_phases(g);
-  int e0 = -1, e1 = -1;
-  if (g->timing) PR_TRY(time_mark(g, s, &e0));
-  const bool pend = g->epi_pending;
-  g->epi_pending = false;
-  const HotEpiFn fused = hot_epi_kernel(g->code, g->C, g->epi_walk);
-  if (!fused) return fail(PR_ERR_STATE, "no fused hot + epilogue kernel for this layout");
-  const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
-  const EpiArgs ea{g->nblk, (g->pend_pbuf ? g->partial2 : g->partial).as<double>(), g->rmask.p, g->cbase.as<int32_t>(),
-                   g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[g->pend_out].as<double>() + g->own_off,
-                   g->teleport, g->damping, g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
-                   g->x_sbase.as<int32_t>()};
-  for (int c = 0; c < nph; ++c) {
-    if (pend && c + 1 < g->n_echunks) {
-      const int64_t g0 = (int64_t)(c + 1) * g->ep_chunk_groups;
-      hipLaunchKernelGGL(fused, dim3((unsigned)g->hot_grid), dim3(kHotThreads), hot_epi_lds(g->hot), s,
-                         g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
-                         partial_buf(g), g->poff.as<int64_t>(), g->piece_part.as<double>(), g->hpos.as<int32_t>(), c,
-                         g->opts.epi_cus, ea, g->cbuf[g->pend_in].as<double>(), g->slots, (double)g->V, g0,
-                         g0 + g->ep_chunk_groups, g->ectr.as<unsigned>() + c, g->unit_part.as<double2>() + g->n_units,
-                         PackDst{});
-      PR_HIP(hipGetLastError());
-      if (c + 1 == g->n_echunks - 1)  // the last chunk of i - 1 is out: its finalize (dc of i)
-        PR_TRY(launch_finalize(g, g->n_long, g->unit_part.as<double2>(), g->n_units + epi_groups(g), g->pend_in,
-                               g->pend_out, s));
-    } else {
-      PR_TRY(launch_hot(g, in, c, c + 1));
-    }
-  }
-  if (g->n_segs > 0)
-    hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
-                       g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
-                       partial_buf(g));
-  PR_TRY(launch_epi_range(g, 0, g->ep_chunk_groups, g->pbuf, in, out));
-  g->epi_pending = true;
-  g->pend_in = in;
-  g->pend_out = out;
-  g->pend_pbuf = g->pbuf;
-  if (g->timing) {
-    PR_TRY(time_mark(g, s, &e1));
-    g->spmv_ev.push_back({e0, e1});
-    g->iter_ev.push_back({e0, e1});
-    ++g->spmv_passes;
-  }
-  g->pbuf ^= 1;
-  g->cur = out;
-  ++g->iters_done;
-  return PR_OK;
-}
-
 int iter_compute(pr_graph *g) {
-  if (g->epi_overlap) return iter_compute_overlap(g);
   hipStream_t s = g->stream;
   const int64_t own = g->own_off;
   const int in = g->cur, out = g->cur ^ 1;
@@ -474,7 +364,7 @@ int iter_compute(pr_graph *g) {
     if (g->n_segs > 0)
       hipLaunchKernelGGL(k_seg_reduce, dim3(grid_for(g->n_segs, kThreads / kWave, 4096)), dim3(kThreads), 0, s,
                          g->n_segs, g->seg_slot.as<int64_t>(), g->seg_p0.as<int32_t>(), g->piece_part.as<double>(),
-                         partial_buf(g));
+                         g->partial.as<double>());
     const EpiGrpFn epi = epi_grp_kernel(g->C, g->epi_walk, g->epi_narrow);
     PackDst pd{};  // fused pack: c' straight into the send runs paired with buffer `out`
     if (g->x_fused) {
@@ -484,7 +374,7 @@ int iter_compute(pr_graph *g) {
       for (int q = 0; q < g->nparts; ++q) pd.soff[q] = g->x_soff[q];
     }
     hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
-                       g->nblk, (int64_t)0, (g->nblk + kEpiGroup - 1) / kEpiGroup, partial_buf(g), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
+                       g->nblk, (int64_t)0, (g->nblk + kEpiGroup - 1) / kEpiGroup, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
                        g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
                        (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
                        g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
@@ -504,10 +394,6 @@ int iter_compute(pr_graph *g) {
 int iter_step(pr_graph *g, int32_t iterations) {
   if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
   if (g->grouped) return fail(PR_ERR_STATE, "graph belongs to a group: use pr_group_step");
-  if (g->epi_overlap) {  // P = 1: no exchange; the pass records its own intervals
-    for (int32_t it = 0; it < iterations; ++it) PR_TRY(iter_compute(g));
-    return PR_OK;
-  }
   for (int32_t it = 0; it < iterations; ++it) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g->timing) {

@@ -807,7 +807,7 @@ __device__ __forceinline__ uint64_t class_range_mask(int x0, int x1) {
 // -- and the sums are bitwise those of the class loop (whose absent classes add an exact +0).
 // (at least 4 waves per SIMD: the LDS of four four-wave workgroups per CU)
 
-// The arguments of the grouped epilogue (k_epilogue_grp, k_spmv_hot_epi); the fused-pack target
+// The arguments of the grouped epilogue (k_epilogue_grp); the fused-pack target
 // (an array indexed by peer) stays a kernel argument, passed on by reference (a local copy of it
 // would be indexed in scratch).
 struct EpiArgs {
@@ -827,21 +827,12 @@ struct EpiArgs {
 // One group gi (kEpiGroup consecutive 64-row blocks) of the grouped epilogue, by one wave with its
 // LDS window win (kEpiWin slots + the zero slot win[kEpiWin]).  The group's dangling and L1
 // partials go to ep_part[gi] (a fixed-order wave sum), so k_finalize adds the same values in the
-// same order whichever wave, workgroup or launch ran the group: every epilogue schedule (one
-// pass, chunks on a second stream, epilogue waves inside k_spmv_hot_epi) is bitwise the same.
-// The body of k_epilogue_grp (below) and of k_spmv_hot_epi's epilogue waves.
-//
-// NT (k_spmv_hot_epi, PR_EPI_NT): every load and store of the group is non-temporal (LDS-DMA with
-// the nt policy, aux = 2), so the streamed partial runs and row data do not evict the class
-// region the hot phase running beside it gathers from its XCD's L2.
-template <int C, bool WALK, bool NT = false>
+// same order whichever wave, workgroup or launch ran the group: every epilogue schedule and grid
+// shape is bitwise the same (round 4's overlapped-epilogue schedules relied on it; they were
+// measured slower and removed, profiles/r04/README.md).  The body of k_epilogue_grp (below).
+template <int C, bool WALK>
 __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, int64_t gi, double tdc, double *win,
                                           double2 *__restrict__ ep_part) {
-  constexpr int kAux = NT ? 2 : 0;
-  auto ld = [](const auto *p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
-  };
   double dcp = 0.0, l1p = 0.0;
   constexpr int G = kEpiGroup, W = kEpiWin;
   constexpr int MW = mask_words<C>();  // 32-bit mask words per row
@@ -858,22 +849,22 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     const int64_t L = (b0 + g) * kWave + lane;
     const bool ok = g < nb;
     if constexpr (MW == 4) {
-      const pr_v4i q = ok ? ld(static_cast<const pr_v4i *>(a.rmask) + L) : pr_v4i{0, 0, 0, 0};
-      mw[0][g] = (uint32_t)q.x, mw[1][g] = (uint32_t)q.y, mw[2][g] = (uint32_t)q.z, mw[3][g] = (uint32_t)q.w;
+      const uint4 q = ok ? static_cast<const uint4 *>(a.rmask)[L] : make_uint4(0u, 0u, 0u, 0u);
+      mw[0][g] = q.x, mw[1][g] = q.y, mw[2][g] = q.z, mw[3][g] = q.w;
     } else if constexpr (MW == 2) {
-      const uint64_t q = ok ? ld(static_cast<const uint64_t *>(a.rmask) + L) : 0ull;
-      mw[0][g] = (uint32_t)q, mw[1][g] = (uint32_t)(q >> 32);
+      const uint2 q = ok ? static_cast<const uint2 *>(a.rmask)[L] : make_uint2(0u, 0u);
+      mw[0][g] = q.x, mw[1][g] = q.y;
     } else {
-      mw[0][g] = ok ? ld(static_cast<const uint32_t *>(a.rmask) + L) : 0u;
+      mw[0][g] = ok ? static_cast<const uint32_t *>(a.rmask)[L] : 0u;
     }
-    info[g] = ok ? ld(a.rowinfo + L) : kRowHole;
-    rold[g] = ok ? ld(a.r + L) : 0.0;
+    info[g] = ok ? a.rowinfo[L] : kRowHole;
+    rold[g] = ok ? a.r[L] : 0.0;
     S[g] = 0.0;
   }
   // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
   // per class with v_readlane
-  const int cs = lane < C ? ld(a.cbase + b0 * C + lane) : 0;
-  const int ce = lane < C ? ld(a.cbase + (b0 + nb) * C + lane) : 0;
+  const int cs = lane < C ? a.cbase[b0 * C + lane] : 0;
+  const int ce = lane < C ? a.cbase[(b0 + nb) * C + lane] : 0;
   if constexpr (C <= kWave) {
     // lane y: class y's run start rounded down to 16 bytes (sa), its staged length n2 (0: no
     // slots in this group) and its window position, the exclusive prefix of n2 over the
@@ -896,13 +887,13 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
           const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
           double *dst = win + __builtin_amdgcn_readlane(pre, y);
           for (int o = 0; o < n; o += 2 * kWave)
-            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, kAux);
+            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
         }
         const int Tb = __builtin_amdgcn_readlane(incl, C - 1);  // staged slots (even)
         const int nl = (__builtin_amdgcn_readlane(sincl, C - 1) + 7) >> 3;  // 16-byte lanes of positions
         const double *esrc = reinterpret_cast<const double *>(a.epos + eo);
         for (int o = 0; o < nl; o += kWave)
-          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, kAux);
+          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
         __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
         const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
         int acc = 0;  // index of block g's first position
@@ -930,7 +921,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
         double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
         for (int o = 0; o < n; o += 2 * kWave)
-          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, kAux);
+          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
       for (int y = x0; y < x1; ++y) {
@@ -962,7 +953,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         if (xe > x && fill + n2 > W) break;
         const double *src = a.partial + sa;
         for (int o = 0; o < n2; o += 2 * kWave)
-          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, kAux);
+          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
         fill += n2;
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
@@ -995,13 +986,11 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     const double rn = affine(Sv, tdc, a.teleport, a.damping);
     double cn = 0.0;
     if (!(info[g] & kRowHole)) {
-      if constexpr (NT) __builtin_nontemporal_store(rn, a.r + L);
-      else a.r[L] = rn;
+      a.r[L] = rn;
       const uint32_t d = info[g] & kRowDegMask;
       if (d > 0) {
         cn = __ddiv_rn(rn, (double)d);
-        if constexpr (NT) __builtin_nontemporal_store(cn, a.cout + L);
-        else a.cout[L] = cn;
+        a.cout[L] = cn;
       } else if (info[g] & kRowSink) {
         dcp = __dadd_rn(dcp, rn);
       }
@@ -1025,7 +1014,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
 }
 
 //
-// Groups [g_lo, g_hi) only: the whole pass, or one chunk of the overlapped epilogue (PR_BOPT_EPI_OVERLAP).
+// Groups [g_lo, g_hi) of the pass (all of them in the product).
 template <int C, bool WALK, int NT>
 __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
     int64_t nblk, int64_t g_lo, int64_t g_hi, const double *__restrict__ partial, const void *__restrict__ rmask_v,
@@ -1045,89 +1034,6 @@ __global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
   const double tdc = dc_from_slots(cin, sp) / n_vertices;
   const int64_t nw = (int64_t)gridDim.x * NW;
   for (int64_t gi = g_lo + (int64_t)blockIdx.x * NW + wv; gi < g_hi; gi += nw) epi_group<C, WALK>(a, pd, gi, tdc, win, ep_part);
-}
-
-// Phase ph of k_spmv_hot for iteration i + 1 with epilogue chunk ph + 1 of iteration i beside it, in
-// one launch (PR_BOPT_EPI_OVERLAP; P = 1, compact codes).  k_spmv_hot is bound by its CU's vector-
-// memory path (the divergent gathers keep the address unit ~96 % busy) and the epilogue by HBM
-// streaming (LDS-DMA of the partial runs), so the two get DIFFERENT CUs: one 1024-thread workgroup
-// per CU as k_spmv_hot, and on every XCD the last `epi_cus` workgroups (grid slots b / 8 >= 32 -
-// epi_cus) run epilogue groups with 16 waves of 8 KiB windows while the others run the phase's
-// wave units as k_spmv_hot's teams.  (Epilogue waves placed beside the hot waves of the same CU
-// took 2.8x the phase: their loads queue behind the gathers at the CU's address unit,
-// profiles/r04/README.md.)  Groups come from a device counter (ectr, zeroed by k_finalize each
-// iteration), and a hot workgroup that has finished its units reuses its LDS as 16 windows and
-// takes groups too, so whichever side finishes first helps the other's tail.  The epilogue reads
-// the partial buffer the previous hot pass wrote (ea.partial) while this phase writes the other
-// one, and it touches only the rows (r, c') of its chunk, which no hot phase of this launch reads.
-// Group partials go to ep_part[gi] (epi_group): the sums are bitwise those of the one-pass epilogue.
-#ifndef PR_EPI_NT
-#define PR_EPI_NT 1
-#endif
-template <int C, bool WALK>
-__device__ __forceinline__ void epi_groups_dynamic(const EpiArgs &ea, const PackDst &pd, int64_t g_lo, int64_t g_hi,
-                                                   unsigned *ectr, double tdc, double *win, double2 *ep_part) {
-  const int lane = lane_id();
-  if (lane == 0) win[kEpiWin] = 0.0;  // the zero slot
-  unsigned t = 0;
-  if (lane == 0) t = atomicAdd(ectr, 1u);
-  while (true) {
-    const int64_t gi = g_lo + (int64_t)__builtin_amdgcn_readfirstlane((int)t);
-    if (gi >= g_hi) break;
-    if (lane == 0) t = atomicAdd(ectr, 1u);  // the next group's ticket, in flight during this group
-    epi_group<C, WALK, PR_EPI_NT != 0>(ea, pd, gi, tdc, win, ep_part);
-  }
-}
-
-template <int CODE, int C, bool WALK>
-__global__ __launch_bounds__(kHotThreads) void k_spmv_hot_epi(
-    const Unit *__restrict__ units, const int64_t *__restrict__ ucum, HotGeom hg, CodeSrc cd,
-    const double *__restrict__ cin, double *__restrict__ partial, const int64_t *__restrict__ poff,
-    double *__restrict__ piece_part, const int32_t *__restrict__ hpos, int ph, int epi_cus, EpiArgs ea,
-    const double *__restrict__ ecin, SlotPos sp, double n_vertices, int64_t g_lo, int64_t g_hi,
-    unsigned *__restrict__ ectr, double2 *__restrict__ ep_part, PackDst pd) {
-  static_assert(CODE == kCodeC20 || CODE == kCodeC24, "one part, compact codes");
-  extern __shared__ double hot[];
-  const int wv = __builtin_amdgcn_readfirstlane(wave_id());
-  const int nteams = (int)(gridDim.x / kXcds) - epi_cus, team = (int)(blockIdx.x / kXcds);
-  double *win = hot + wv * (kEpiWin + 2);  // an epilogue wave's window (after the hot work, for hot teams)
-  const double tdc = dc_from_slots(ecin, sp) / n_vertices;
-  if (team >= nteams) {  // an epilogue CU
-    epi_groups_dynamic<C, WALK>(ea, pd, g_lo, g_hi, ectr, tdc, win, ep_part);
-    return;
-  }
-  ClassSrc cs;
-  cs.zb = (uint32_t)hg.slots() * 8u;
-  cs.hb = (uint32_t)(hg.q_load + 1) * 8u;
-  cs.tbl = nullptr;
-  double *stage = hot + hg.stage_off() + wv * kStageSlots;
-  const int x = (int)(blockIdx.x % kXcds) + kXcds * ph;
-  const int64_t first = (int64_t)x * hg.Q_pad + hg.q_load;  // region index q_load + 1 + k -> x*Q_pad + q_load + k
-  cs.crs = __builtin_amdgcn_make_buffer_rsrc((void *)(cin + first), 0, (uint32_t)((hg.Q_pad - hg.q_load) * 8),
-                                             0x00020000);
-  stage_hot_set<false, true>(hg, x, hpos, nullptr, cin, hot, nullptr);
-  __syncthreads();
-  hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
-  __syncthreads();  // every wave is done with the hot set: its LDS becomes 16 epilogue windows
-  epi_groups_dynamic<C, WALK>(ea, pd, g_lo, g_hi, ectr, tdc, win, ep_part);
-}
-
-using HotEpiFn = void (*)(const Unit *, const int64_t *, HotGeom, CodeSrc, const double *, double *, const int64_t *,
-                          double *, const int32_t *, int, int, EpiArgs, const double *, SlotPos, double, int64_t, int64_t,
-                          unsigned *, double2 *, PackDst);
-template <int CODE>
-inline HotEpiFn hot_epi_kernel_code(int C, bool walk) {
-  switch (C) {
-    case 16: return walk ? k_spmv_hot_epi<CODE, 16, true> : k_spmv_hot_epi<CODE, 16, false>;
-    case 32: return walk ? k_spmv_hot_epi<CODE, 32, true> : k_spmv_hot_epi<CODE, 32, false>;
-    case 64: return walk ? k_spmv_hot_epi<CODE, 64, true> : k_spmv_hot_epi<CODE, 64, false>;
-    default: return nullptr;
-  }
-}
-inline HotEpiFn hot_epi_kernel(int code, int C, bool walk) {
-  if (code == kCodeC20) return hot_epi_kernel_code<kCodeC20>(C, walk);
-  if (code == kCodeC24) return hot_epi_kernel_code<kCodeC24>(C, walk);
-  return nullptr;
 }
 
 // Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks.
