@@ -84,6 +84,8 @@ def test_plain_bench_gpus_2_runs_two_ranks():
     assert line["n_gpus"] == 2 and line["value"] is not None
     assert line["parity"]["ranks_from"] == "2 rank(s)" and line["parity"]["every_row_owned_once"] is True
     assert line["parity"]["max_rel"] <= RANK_TOL
+    # the oracle built its own CSR from the raw edges, and the library's canonical CSR equals it
+    assert line["parity"]["csr_bit_exact"] is True
 
 
 @pytest.mark.gpu
