@@ -176,7 +176,10 @@ constexpr __host__ __device__ bool code_is_piece(int code) { return code >= kCod
 // more 0.0 slot (where compact cold entries point their LDS read), the workgroup's unit counter,
 // then one staging window of kStageSlots segment sums per wave (16 KiB in all; 128 beat 256 by
 // ~0.5 % and 64 by ~0.8 % at R-MAT s26, profiles/r01/stage_ab/).
-constexpr int kStageSlots = 128;
+#ifndef PR_STAGE_SLOTS  // A/B builds only (tools/ab_build.sh): the library reads no environment
+#define PR_STAGE_SLOTS 128
+#endif
+constexpr int kStageSlots = PR_STAGE_SLOTS;
 constexpr int kHotLdsBytes = 160 * 1024;
 constexpr int kHotSlotsMax = (kHotLdsBytes - (kHotThreads / 64) * kStageSlots * 8) / 8 - 3;
 constexpr int kHotSlotsDefault = kHotSlotsMax;  // 18429 hot contributions (144 KiB)
