@@ -414,6 +414,11 @@ __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs)
   else return b8 - cs.hb;
 }
 
+// Cache policy of the cold gathers (aux bits of the buffer load); A/B builds only.
+#ifndef PR_GATHER_AUX
+#define PR_GATHER_AUX 0
+#endif
+
 // The unit's values: per entry an LDS read (hot) and a range-checked gather-space load (cold),
 // one of them an exact 0.
 template <bool PIECE>
@@ -425,7 +430,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodes &w, const doubl
     const uint32_t la = (int32_t)c < 0 ? 0u : c;
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
     const uint32_t go = c ^ kEntGlobal;  // LDS codes become offsets >= 2^31: out of range, no request
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, go, 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, go, 0, PR_GATHER_AUX));
     v[j] = __dadd_rn(a, b);
   }
 }
@@ -439,7 +444,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, PR_GATHER_AUX));
     v[j] = __dadd_rn(a, b);
   }
 }
@@ -454,7 +459,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, 0));
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, PR_GATHER_AUX));
     v[j] = __dadd_rn(a, b);
   }
 }
