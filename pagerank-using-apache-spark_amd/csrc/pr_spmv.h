@@ -829,6 +829,11 @@ struct EpiArgs {
   const int32_t *sbase;
 };
 
+// Cache policy of the epilogue's LDS-DMA of the partial runs (aux bits); A/B builds only.
+#ifndef PR_EPI_DMA_AUX
+#define PR_EPI_DMA_AUX 0
+#endif
+
 // One group gi (kEpiGroup consecutive 64-row blocks) of the grouped epilogue, by one wave with its
 // LDS window win (kEpiWin slots + the zero slot win[kEpiWin]).  The group's dangling and L1
 // partials go to ep_part[gi] (a fixed-order wave sum), so k_finalize adds the same values in the
@@ -892,13 +897,13 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
           const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
           double *dst = win + __builtin_amdgcn_readlane(pre, y);
           for (int o = 0; o < n; o += 2 * kWave)
-            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+            if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, PR_EPI_DMA_AUX);
         }
         const int Tb = __builtin_amdgcn_readlane(incl, C - 1);  // staged slots (even)
         const int nl = (__builtin_amdgcn_readlane(sincl, C - 1) + 7) >> 3;  // 16-byte lanes of positions
         const double *esrc = reinterpret_cast<const double *>(a.epos + eo);
         for (int o = 0; o < nl; o += kWave)
-          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, 0);
+          if (o + lane < nl) __builtin_amdgcn_global_load_lds(esrc + 2 * (o + lane), win + Tb + 2 * o, 16, 0, PR_EPI_DMA_AUX);
         __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
         const uint16_t *ep = reinterpret_cast<const uint16_t *>(win + Tb);
         int acc = 0;  // index of block g's first position
@@ -926,7 +931,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
         double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
         for (int o = 0; o < n; o += 2 * kWave)
-          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, 0);
+          if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, PR_EPI_DMA_AUX);
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
       for (int y = x0; y < x1; ++y) {
@@ -958,7 +963,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         if (xe > x && fill + n2 > W) break;
         const double *src = a.partial + sa;
         for (int o = 0; o < n2; o += 2 * kWave)
-          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, 0);
+          if (o + 2 * lane < n2) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, win + fill + o, 16, 0, PR_EPI_DMA_AUX);
         fill += n2;
       }
       __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt = lgkmcnt = 0)
