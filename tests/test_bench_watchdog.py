@@ -69,3 +69,18 @@ def test_plain_gpus_n_launches_n_ranks():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["value"] is None and "GPU" in d["error"], d
     assert "starting 2 ranks" in p.stderr
+
+
+def test_gather_roofline_block():
+    """roofline.gather: cold gathers / the measured L2-resident gather rate and
+    LDS-served entries / the measured LDS rate, against the pass time (profiles/rates.json)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    rates = bench.gather_rates()
+    assert rates is not None and rates["l2_gather_per_s"] > 1e11 and rates["lds_read_per_s"] > 1e12
+    g = bench.gather_roofline({"local_edges": 1_000_000_000, "hot_cover_ppm": 750_000}, 2.0)
+    assert g["cold_gathers"] == 250_000_000 and g["lds_entries"] == 750_000_000
+    assert abs(g["cold_floor_ms"] - 250e6 / rates["l2_gather_per_s"] * 1e3) < 1e-3
+    assert abs(g["frac_cold"] - g["cold_floor_ms"] / 2.0) < 1e-3
+    assert bench.gather_roofline({"local_edges": 10, "hot_cover_ppm": 0}, 0.0) is None
