@@ -32,8 +32,10 @@ Rank 0 prints ONE JSON line (the driver's contract), including
   exchange_overlap_ab (N > 1): a calibration before the timed region runs max(5, K/2) steps
                   with the exchange after the pass (the library default) and overlapped with the
                   next iteration's SpMV phases (pr_set_option) with 0/1/2 CUs per XCD kept free for
-                  the transfer kernels; the fastest mode is the one timed (config.exchange_mode);
-                  the parity leg checks both exchange modes.
+                  the transfer kernels, and -- when every rank can map its peers' buffers -- the
+                  CU-free IPC transport (copy-engine pulls, unchunked and chunked); the fastest mode
+                  is the one timed (config.exchange_mode); the parity leg checks the RCCL modes and
+                  the IPC transport (bitwise against RCCL: parity.ipc_bitwise_equal_rccl).
   --share-device: a rehearsal of the N > 1 path on a box with fewer GPUs than ranks (every rank
                   on device rank % count, RCCL over loopback sockets via a per-rank NCCL_HOSTID);
                   config.shared_device_rehearsal marks such a line: its parity is real, its speed
@@ -402,7 +404,8 @@ def main() -> int:
     # configuration timed below; every mode's calibration time is reported (exchange_overlap_ab)
     # and the parity leg checks both exchange modes
     overlap = None
-    mode = ("unchunked", False, 0)
+    mode = ("unchunked", False, 0, False)
+    ipc_ok = False
     if dist is not None and info.get("classes", 1) >= 16 and not a.no_overlap_ab:
         def cal_steps(k):
             g.reset()
@@ -423,15 +426,30 @@ def main() -> int:
         k_cal = max(5, a.steps // 2)
         overlap = {"calibration_steps": k_cal, "chunks": info.get("classes", 1) // 8, "library_default": "unchunked"}
         best = None
-        for name, chunked, reserve in (("unchunked", False, 0), ("chunked_reserve0", True, 0),
-                                       ("chunked_reserve1", True, 1), ("chunked_reserve2", True, 2)):
+        modes = [("unchunked", False, 0, False), ("chunked_reserve0", True, 0, False),
+                 ("chunked_reserve1", True, 1, False), ("chunked_reserve2", True, 2, False)]
+        # the CU-free transport (PR_OPT_XCHG_IPC): the copy engines pull the runs out of the peers'
+        # IPC-mapped send buffers; its set-up is collective and fails on every rank alike
+        try:
+            g.set_exchange_ipc(True)
+            g.set_exchange_ipc(False)
+            ipc_ok = True
+            modes += [("ipc_unchunked", False, 0, True), ("ipc_chunked", True, 0, True)]
+        except Exception as e:
+            overlap["ipc_error"] = str(e)
+            log(f"IPC exchange unavailable: {e}")
+        for name, chunked, reserve, ipc in modes:
+            if ipc_ok:
+                g.set_exchange_ipc(ipc)
             g.set_exchange_chunks(chunked)
             g.set_hot_reserve(reserve)
             ms = cal_steps(k_cal)
             overlap[f"{name}_ms_per_step"] = ms
             if best is None or ms < best[0]:
-                best = (ms, (name, chunked, reserve))
+                best = (ms, (name, chunked, reserve, ipc))
         mode = best[1]
+        if ipc_ok:
+            g.set_exchange_ipc(mode[3])
         g.set_exchange_chunks(mode[1])
         g.set_hot_reserve(mode[2])
         overlap["chosen"] = mode[0]
@@ -502,14 +520,21 @@ def main() -> int:
                 del rt, own
             return mine, owned_once
 
-        g.set_hot_reserve(0)  # results do not depend on it (bitwise tested); both exchange modes
+        g.set_hot_reserve(0)  # results do not depend on it (bitwise tested); every exchange mode
+        if ipc_ok:
+            g.set_exchange_ipc(False)
         g.set_exchange_chunks(False)
         mine, owned_once = gpu_ranks()
-        mine_chunked = None
+        mine_chunked = mine_ipc = None
         if overlap is not None:
             g.set_exchange_chunks(True)
             mine_chunked, oc = gpu_ranks()
             owned_once = owned_once and oc
+            if ipc_ok:  # the IPC transport (chunked) must give bitwise the RCCL transport's ranks
+                g.set_exchange_ipc(True)
+                mine_ipc, oc = gpu_ranks()
+                owned_once = owned_once and oc
+                g.set_exchange_ipc(False)
             g.set_exchange_chunks(False)
         if rank == 0:
             try:
@@ -524,6 +549,10 @@ def main() -> int:
                 if mine_chunked is not None:
                     parity["max_rel_overlapped_exchange"] = float(np.max(np.abs(mine_chunked - ref) / ref))
                     parity["max_rel"] = max(parity["max_rel"], parity["max_rel_overlapped_exchange"])
+                if mine_ipc is not None:
+                    parity["max_rel_ipc_exchange"] = float(np.max(np.abs(mine_ipc - ref) / ref))
+                    parity["ipc_bitwise_equal_rccl"] = bool(np.array_equal(mine_ipc, mine_chunked))
+                    parity["max_rel"] = max(parity["max_rel"], parity["max_rel_ipc_exchange"])
                 if world == 1 and K >= 2:
                     it_ms = res["iter_ms"][1:]
                     med = float(np.median(it_ms))
@@ -563,7 +592,9 @@ def main() -> int:
                 "n_vertices": V,
                 "n_edges_raw": E,
                 "n_edges_dedup": n_edges,
-                "parallelism": f"row-partition x{world}" + (xchg_desc if world > 1 else ""),
+                "parallelism": f"row-partition x{world}" + (
+                    (" + copy-engine pulls from IPC-mapped peer send runs" if mode[3] else xchg_desc)
+                    if world > 1 else ""),
                 "exchange_mode": mode[0] if world > 1 else None,
                 "exchange_doubles_per_iter_rank0": info.get("xchg_send", 0) if world > 1 else 0,
                 "iterations_timed": a.steps,

@@ -179,6 +179,12 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 /* PR_OPT_HOT_RESERVE: CUs per XCD that the heavy SpMV kernel leaves free (0..3, default 0), for
  * the overlapped exchange's transfer kernels, which cannot share a CU with it (LDS, registers). */
 #define PR_OPT_HOT_RESERVE 2
+/* PR_OPT_XCHG_IPC (RCCL path, ranks on one node): 1 = every rank pulls the runs it reads straight
+ * out of its peers' send buffers (IPC-mapped) with the copy engines, ordered by interprocess
+ * events, so no transfer kernel takes a CU from the SpMV; 0 = RCCL send/recv (the default).
+ * Collective like PR_OPT_XCHG_CHUNKS (which it combines with); the first enable maps the peers'
+ * buffers and fails with PR_ERR_COMM on every rank if any rank cannot. */
+#define PR_OPT_XCHG_IPC 3
 int pr_set_option(pr_graph *g, int32_t option, int64_t value);
 
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes

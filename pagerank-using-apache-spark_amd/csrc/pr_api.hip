@@ -294,6 +294,10 @@ int pr_set_option(pr_graph *g, int32_t option, int64_t value) {
     if (g->C > 1) PR_TRY(pr::set_hot_reserve(g, (int)value));
     return PR_OK;
   }
+  if (option == PR_OPT_XCHG_IPC) {
+    if (value != 0 && value != 1) return fail(PR_ERR_INVALID, "PR_OPT_XCHG_IPC: 0 (RCCL) or 1 (IPC copy engines)");
+    return pr::set_exchange_ipc(g, value == 1);
+  }
   if (option != PR_OPT_XCHG_CHUNKS) return fail(PR_ERR_INVALID, "unknown option");
   PR_TRY(pr::join_exchange(g));  // a pending overlapped exchange finishes under the old setting
   g->x_chunked = value != 0 && g->n_xc > 1;
@@ -509,6 +513,7 @@ void pr_graph_destroy(pr_graph *g) {
   DeviceGuard dg(g->device);
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->xstream) (void)hipStreamSynchronize(g->xstream);
+  pr::ipc_destroy(g);  // after the peers' last copies out of this part's send runs
   if (g->comm) (void)ncclCommDestroy(g->comm);
   for (hipEvent_t e : g->ev_pool) (void)hipEventDestroy(e);
   if (g->xev) (void)hipEventDestroy(g->xev);

@@ -362,6 +362,7 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
     if (ev_b) PR_HIP(hipEventRecord(ev_b, g->stream));
     return PR_OK;
   }
+  if (g->x_ipc) return exchange_ipc(g, buf, ev_a, ev_b);  // copy engines out of the peers' runs
   if (g->x_packed != buf) PR_TRY(exchange_pack(g, buf));  // else the epilogue wrote the runs
   g->x_packed = -1;
   PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));

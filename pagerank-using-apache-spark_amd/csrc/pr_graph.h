@@ -31,6 +31,10 @@
 
 #include "pr_internal.h"
 
+namespace pr {
+struct IpcState;  // pr_ipc.hip
+}
+
 // Build options (include/pagerank_hip.h PR_BOPT_*): the library reads no environment variables.
 struct pr_build_opts {
   int classes = 0;       // 0: the size policy
@@ -160,6 +164,11 @@ struct pr_graph {
   pr::DevBuf x_pmask, x_sbase;
   int x_packed = -1;
 
+  // CU-free transport of the RCCL path (PR_OPT_XCHG_IPC, pr_ipc.hip): every rank pulls its runs out
+  // of its peers' IPC-mapped send buffers with the copy engines
+  pr::IpcState *ipc = nullptr;  // mapped on first use, kept until destroy
+  bool x_ipc = false;           // exchanges use it
+
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_size = 1;
@@ -199,6 +208,12 @@ int exchange(pr_graph *g, int buf, hipEvent_t ev_a = nullptr, hipEvent_t ev_b = 
 double *send_runs(const pr_graph *g, int buf);  // the packed send runs paired with gather buffer buf
 int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
+// IPC transport (pr_ipc.hip): collective switch; the reuse wait before the send runs of buf are
+// written (no-op unless x_ipc); the exchange itself; unmapping at destroy
+int set_exchange_ipc(pr_graph *g, bool on);
+int ipc_send_runs_free(pr_graph *g, int buf);
+int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b);
+void ipc_destroy(pr_graph *g);
 hipEvent_t next_event(pr_graph *g);  // the next timing event of g's pool (nullptr: creation failed)
 int time_mark(pr_graph *g, hipStream_t s, int *index);  // records one on s; *index into ev_pool
 }  // namespace pr

@@ -1,0 +1,394 @@
+// CU-free exchange for the RCCL path (PR_OPT_XCHG_IPC): one process per GPU on
+// one node, every rank pulls the runs its in-links read straight out of its peers' send buffers
+// with the copy engines, so no transfer kernel competes with k_spmv_hot for a CU.
+//
+// Replaces the same per-iteration re-shuffle as exchange() (Sparky.java:192's join of the links
+// with the ranks), with the same runs, chunks and gather-space positions; only the transport and
+// its completion signals differ:
+//   memory   every rank's double-buffered send runs (x_sbuf) are mapped into every peer
+//            (hipIpcGetMemHandle / hipIpcOpenMemHandle); a receiver copies run q -> its gather space
+//            with hipMemcpyDeviceToDeviceNoCU on its xstream, chunk by chunk (x_ev[c] as before).
+//   device   two interprocess events per buffer b and rank: `sent[b]` (recorded on the owner's
+//            compute stream once the runs of b are written: fused epilogue + k_finalize, or k_pack)
+//            and `copied[b]` (recorded on the owner's xstream after its copies out of every peer's
+//            runs of b).  A receiver's xstream waits for every peer's sent[b] before copying; an
+//            owner's compute stream waits for every peer's copied[b] of the previous exchange of b
+//            before it writes the runs of b again (the reuse hazard of the double buffer).
+//   host     a wait on an interprocess event binds to the latest record *enqueued so far*, so the
+//            waiter's host must not enqueue it before the owner's host has enqueued the record it
+//            means.  Every rank publishes, in a small shared-memory page of its own, how many
+//            sent[b] / copied[b] records it has enqueued; a waiter spins on its host until the
+//            owner's count reaches the exchange it needs, then enqueues the stream wait.  No device
+//            work ever waits for a record that is not already enqueued, and the hosts stay at most
+//            one exchange apart per buffer, so a later record of the same event cannot be taken for
+//            the one meant (its owner would first have had to pass a wait on this rank).  A host
+//            spin that exceeds kSpinLimit fails with PR_ERR_COMM instead of hanging.
+// Set-up and switching are collective (pr_set_option on every rank): handles and page names travel
+// by ncclAllGather over the attached communicator, and every rank agrees on success with an
+// ncclAllReduce before the mode is used.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pr_graph.h"
+
+namespace pr {
+
+int exchange_pack(pr_graph *g, int buf);  // pr_exchange.hip
+int64_t send_stride(const pr_graph *g);   // pr_exchange.hip
+
+namespace {
+
+constexpr double kSpinLimit = 120.0;  // seconds a host waits for a peer's record before failing
+
+// one rank's shared-memory page: how many sent[b] / copied[b] records it has enqueued
+struct alignas(64) IpcCounters {
+  std::atomic<int64_t> sent[2];
+  std::atomic<int64_t> copied[2];
+};
+static_assert(std::atomic<int64_t>::is_always_lock_free, "cross-process counters must be lock-free");
+
+// what every rank publishes at set-up (ncclAllGather of bytes)
+struct IpcRecord {
+  hipIpcMemHandle_t mem;         // its x_sbuf
+  hipIpcEventHandle_t sent[2];   // its sent[b]
+  hipIpcEventHandle_t copied[2];  // its copied[b]
+  char page[64];                 // its counter page (shm_open name)
+  int64_t stride;                // doubles per send buffer (send_stride)
+  int64_t soff[kMaxParts + 1];   // its send-run offsets
+  int32_t ok;                    // its local set-up succeeded
+  int32_t pad;
+};
+
+}  // namespace
+
+struct IpcState {
+  int P = 0, self = 0;
+  char page[64] = {0};
+  IpcCounters *mine = nullptr;
+  std::vector<IpcCounters *> peer;    // mapped counter pages (nullptr: self / not opened)
+  std::vector<void *> peer_sbuf;      // mapped send buffers
+  std::vector<int64_t> peer_stride;   // doubles per peer send buffer
+  std::vector<int64_t> peer_soff_me;  // start of the peer's run for this rank
+  hipEvent_t sent[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> peer_sent, peer_copied;  // [q * 2 + b]
+  int64_t n[2] = {0, 0};      // exchanges of buffer b since the mode was (re)enabled
+  int64_t freed[2] = {0, 0};  // exchange index of b whose send-run writes are already ordered
+};
+
+namespace {
+
+void unmap_page(IpcCounters *c) {
+  if (c) munmap(c, sizeof(IpcCounters));
+}
+
+IpcCounters *map_page(const char *name, bool create) {
+  const int fd = shm_open(name, create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+  if (fd < 0) return nullptr;
+  if (create && ftruncate(fd, sizeof(IpcCounters)) != 0) {
+    close(fd);
+    shm_unlink(name);
+    return nullptr;
+  }
+  void *p = mmap(nullptr, sizeof(IpcCounters), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    if (create) shm_unlink(name);
+    return nullptr;
+  }
+  IpcCounters *c = static_cast<IpcCounters *>(p);
+  if (create) new (c) IpcCounters{};
+  return c;
+}
+
+void free_state(IpcState *s) {
+  if (!s) return;
+  for (size_t q = 0; q < s->peer_sbuf.size(); ++q)
+    if (s->peer_sbuf[q]) (void)hipIpcCloseMemHandle(s->peer_sbuf[q]);
+  for (hipEvent_t e : s->peer_sent)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s->peer_copied)
+    if (e) (void)hipEventDestroy(e);
+  for (int b = 0; b < 2; ++b) {
+    if (s->sent[b]) (void)hipEventDestroy(s->sent[b]);
+    if (s->copied[b]) (void)hipEventDestroy(s->copied[b]);
+  }
+  for (IpcCounters *c : s->peer) unmap_page(c);
+  if (s->mine) {
+    unmap_page(s->mine);
+    shm_unlink(s->page);  // normally unlinked at set-up already
+  }
+  (void)hipGetLastError();
+  delete s;
+}
+
+// host wait until `c` reaches v (a peer's enqueued records); PR_ERR_COMM after kSpinLimit
+int spin_until(const std::atomic<int64_t> &c, int64_t v, const char *what, int peer, double limit = kSpinLimit) {
+  if (c.load(std::memory_order_acquire) >= v) return PR_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; c.load(std::memory_order_acquire) < v; ++i) {
+    if (i < 256) {
+      std::this_thread::yield();
+      continue;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if ((i & 1023) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
+      return fail(PR_ERR_COMM, std::string("IPC exchange: peer ") + std::to_string(peer) + " never enqueued its " +
+                                   what + " record (did every rank make the same calls?)");
+  }
+  return PR_OK;
+}
+
+// every rank's streams are idle and every rank got here (tiny all-reduce on the compute stream)
+int comm_barrier(pr_graph *g, int32_t *flag_inout) {
+  DevBuf d;
+  PR_TRY(d.alloc(sizeof(int32_t)));
+  PR_HIP(hipMemcpyAsync(d.p, flag_inout, sizeof(int32_t), hipMemcpyHostToDevice, g->stream));
+  const ncclResult_t rc = ncclAllReduce(d.p, d.p, 1, ncclInt32, ncclMin, g->comm, g->stream);
+  if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(rc));
+  PR_HIP(hipMemcpyAsync(flag_inout, d.p, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  return PR_OK;
+}
+
+int quiesce(pr_graph *g) {
+  PR_TRY(join_exchange(g));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  if (g->xstream) PR_HIP(hipStreamSynchronize(g->xstream));
+  return PR_OK;
+}
+
+// collective: map every peer's send buffers, events and counter page
+int ipc_setup(pr_graph *g) {
+  const int P = g->nparts, self = g->part;
+  IpcState *s = new (std::nothrow) IpcState();
+  if (!s) return fail(PR_ERR_OOM, "host allocation failed");
+  s->P = P;
+  s->self = self;
+  s->peer.assign(P, nullptr);
+  s->peer_sbuf.assign(P, nullptr);
+  s->peer_stride.assign(P, 0);
+  s->peer_soff_me.assign(P, 0);
+  s->peer_sent.assign(2 * (size_t)P, nullptr);
+  s->peer_copied.assign(2 * (size_t)P, nullptr);
+  std::string why;
+  IpcRecord rec;
+  std::memset(&rec, 0, sizeof(rec));
+  rec.ok = 1;
+  auto local = [&](bool cond, const char *what) {
+    if (!cond && rec.ok) {
+      rec.ok = 0;
+      why = what;
+    }
+    (void)hipGetLastError();
+  };
+  std::snprintf(s->page, sizeof(s->page), "/pr_xipc_%d_%d_%llx", (int)getpid(), self,
+                (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
+  s->mine = map_page(s->page, true);
+  local(s->mine != nullptr, "shm_open of the counter page failed");
+  std::memcpy(rec.page, s->page, sizeof(rec.page));
+  local(hipIpcGetMemHandle(&rec.mem, g->x_sbuf.p) == hipSuccess, "hipIpcGetMemHandle failed");
+  for (int b = 0; b < 2 && rec.ok; ++b) {
+    local(hipEventCreateWithFlags(&s->sent[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&s->copied[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
+          "hipEventCreateWithFlags(hipEventInterprocess) failed");
+    if (rec.ok)
+      local(hipIpcGetEventHandle(&rec.sent[b], s->sent[b]) == hipSuccess &&
+                hipIpcGetEventHandle(&rec.copied[b], s->copied[b]) == hipSuccess,
+            "hipIpcGetEventHandle failed");
+  }
+  rec.stride = send_stride(g);
+  for (int q = 0; q <= P; ++q) rec.soff[q] = g->x_soff[q];
+  // publish
+  std::vector<IpcRecord> all((size_t)P);
+  {
+    DevBuf d;
+    const size_t W = sizeof(IpcRecord);
+    int rv = d.alloc(W * (size_t)(P + 1));
+    if (rv != PR_OK) {
+      free_state(s);
+      return rv;
+    }
+    PR_HIP(hipMemcpyAsync(d.p, &rec, W, hipMemcpyHostToDevice, g->stream));
+    const ncclResult_t rc = ncclAllGather(d.p, (uint8_t *)d.p + W, W, ncclUint8, g->comm, g->stream);
+    if (rc != ncclSuccess) {
+      free_state(s);
+      return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+    }
+    PR_HIP(hipMemcpyAsync(all.data(), (uint8_t *)d.p + W, W * (size_t)P, hipMemcpyDeviceToHost, g->stream));
+    PR_HIP(hipStreamSynchronize(g->stream));
+  }
+  int32_t ok = 1;
+  for (int q = 0; q < P; ++q) ok &= all[q].ok;
+  if (!rec.ok) ok = 0;
+  // open the peers' resources (only if every rank's set-up succeeded)
+  for (int q = 0; q < P && ok; ++q) {
+    if (q == self) continue;
+    const IpcRecord &r = all[q];
+    char name[64];
+    std::memcpy(name, r.page, sizeof(name));
+    name[63] = 0;
+    s->peer[q] = map_page(name, false);
+    if (!s->peer[q]) {
+      ok = 0;
+      why = "shm_open of a peer's counter page failed";
+      break;
+    }
+    if (hipIpcOpenMemHandle(&s->peer_sbuf[q], r.mem, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      (void)hipGetLastError();
+      s->peer_sbuf[q] = nullptr;
+      ok = 0;
+      why = "hipIpcOpenMemHandle failed";
+      break;
+    }
+    for (int b = 0; b < 2 && ok; ++b) {
+      if (hipIpcOpenEventHandle(&s->peer_sent[2 * q + b], r.sent[b]) != hipSuccess ||
+          hipIpcOpenEventHandle(&s->peer_copied[2 * q + b], r.copied[b]) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+        why = "hipIpcOpenEventHandle failed";
+      }
+    }
+    s->peer_stride[q] = r.stride;
+    s->peer_soff_me[q] = r.soff[self];
+    // the peer's run for this rank must be exactly what this rank receives from it
+    if (r.soff[self + 1] - r.soff[self] != g->x_roff[q + 1] - g->x_roff[q]) {
+      ok = 0;
+      why = "a peer's send run disagrees with the receive run";
+    }
+  }
+  // every rank has opened every page: the names can go
+  int32_t agreed = ok;
+  const int rv = comm_barrier(g, &agreed);
+  if (s->mine) shm_unlink(s->page);
+  if (rv != PR_OK) {
+    free_state(s);
+    return rv;
+  }
+  if (!agreed) {
+    free_state(s);
+    return fail(PR_ERR_COMM, "IPC exchange set-up failed on " + std::string(ok ? "a peer" : "this rank") +
+                                 (why.empty() ? std::string() : ": " + why));
+  }
+  g->ipc = s;
+  return PR_OK;
+}
+
+}  // namespace
+
+int set_exchange_ipc(pr_graph *g, bool on) {
+  if (on == g->x_ipc) return PR_OK;
+  if (on) {
+    if (!g->comm || g->comm_size <= 1) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs an attached communicator (P > 1)");
+    if (g->x_allgather) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs the per-peer runs (PR_BOPT_EXCHANGE = 0)");
+  }
+  PR_TRY(quiesce(g));
+  if (on && !g->ipc) PR_TRY(ipc_setup(g));
+  // every rank idle (so no copy out of another's buffers is pending) before the mode changes
+  int32_t one = 1;
+  if (on) {
+    IpcState *s = g->ipc;
+    for (int b = 0; b < 2; ++b) {
+      s->mine->sent[b].store(0, std::memory_order_release);
+      s->mine->copied[b].store(0, std::memory_order_release);
+      s->n[b] = s->freed[b] = 0;
+    }
+  }
+  PR_TRY(comm_barrier(g, &one));
+  g->x_ipc = on;
+  return PR_OK;
+}
+
+// Before the compute stream writes the send runs of `buf` for the next exchange: order the writes
+// after every peer's copies of the previous exchange of `buf`.
+int ipc_send_runs_free(pr_graph *g, int buf) {
+  if (!g->x_ipc) return PR_OK;
+  IpcState *s = g->ipc;
+  const int64_t k = s->n[buf] + 1;  // the exchange these writes belong to
+  if (s->freed[buf] >= k) return PR_OK;
+  if (k > 1) {
+    for (int q = 0; q < s->P; ++q) {
+      if (q == s->self) continue;
+      PR_TRY(spin_until(s->peer[q]->copied[buf], k - 1, "copied", q));
+      PR_HIP(hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + buf], 0));
+    }
+  }
+  s->freed[buf] = k;
+  return PR_OK;
+}
+
+int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
+  IpcState *s = g->ipc;
+  if (g->x_packed != buf) {
+    PR_TRY(ipc_send_runs_free(g, buf));
+    PR_TRY(exchange_pack(g, buf));
+  }
+  g->x_packed = -1;
+  const int64_t k = ++s->n[buf];
+  if (s->freed[buf] < k) return fail(PR_ERR_STATE, "IPC exchange: send runs written without the reuse wait");
+  PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
+  PR_HIP(hipEventRecord(s->sent[buf], g->stream));
+  s->mine->sent[buf].store(k, std::memory_order_release);
+  PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));  // this rank's pass no longer reads cbuf[buf]
+  for (int q = 0; q < s->P; ++q) {
+    if (q == s->self) continue;
+    PR_TRY(spin_until(s->peer[q]->sent[buf], k, "sent", q));
+    PR_HIP(hipStreamWaitEvent(g->xstream, s->peer_sent[2 * q + buf], 0));
+  }
+  if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
+  const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
+  double *base = g->cbuf[buf].as<double>();
+  for (int c = 0; c < steps; ++c) {
+    const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;
+    for (int q = 0; q < s->P; ++q) {
+      if (q == s->self) continue;
+      const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
+      if (r1 <= r0) continue;
+      const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(buf & 1) * s->peer_stride[q] +
+                          s->peer_soff_me[q] + r0;
+      PR_HIP(hipMemcpyAsync(base + g->S_pad + g->x_roff[q] + r0, src, sizeof(double) * (size_t)(r1 - r0),
+                            hipMemcpyDeviceToDeviceNoCU, g->xstream));
+    }
+    PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
+  }
+  PR_HIP(hipEventRecord(s->copied[buf], g->xstream));
+  s->mine->copied[buf].store(k, std::memory_order_release);
+  if (ev_b) PR_HIP(hipEventRecord(ev_b, g->xstream));
+  g->x_pending = true;
+  return PR_OK;
+}
+
+// Destroy: the peers may still be copying out of this rank's send buffers; wait (bounded) for the
+// copies of every exchange this rank published, then unmap everything.
+void ipc_destroy(pr_graph *g) {
+  IpcState *s = g->ipc;
+  if (!s) return;
+  g->ipc = nullptr;
+  g->x_ipc = false;
+  bool waited = false;
+  for (int q = 0; q < s->P; ++q) {
+    if (q == s->self || !s->peer[q]) continue;
+    for (int b = 0; b < 2; ++b) {
+      const int64_t k = s->mine->sent[b].load(std::memory_order_acquire);
+      if (k <= 0) continue;
+      if (spin_until(s->peer[q]->copied[b], k, "copied", q, 10.0) != PR_OK) continue;  // peer gone: nothing to order
+      (void)hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + b], 0);
+      waited = true;
+    }
+  }
+  if (waited) (void)hipStreamSynchronize(g->stream);
+  free_state(s);
+}
+
+}  // namespace pr

@@ -283,6 +283,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
   }
   g->cur = 0;
   g->x_packed = -1;
+  PR_TRY(ipc_send_runs_free(g, 0));  // k_finalize below writes the slots of the runs of buffer 0
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
                      dinit.p ? dinit.as<double>() : nullptr, g->r.as<double>(), g->rowinfo.as<uint32_t>(),
@@ -333,6 +334,7 @@ int iter_compute(pr_graph *g) {
     open_ev = (int)g->ev_next - 1;  // a following interval may start where this one ended
     return PR_OK;
   };
+  PR_TRY(ipc_send_runs_free(g, out));  // the epilogue and k_finalize write the runs of `out`
   const int nph = g->C > 1 ? n_hot_phases(g) : 1;
   const bool phased_wait = g->C > 1 && g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1;
   if (!phased_wait) PR_TRY(join_exchange(g));

@@ -46,6 +46,7 @@ STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "i
 PR_CB_RANKS = 1
 PR_OPT_XCHG_CHUNKS = 1
 PR_OPT_HOT_RESERVE = 2
+PR_OPT_XCHG_IPC = 3
 PR_COMM_ID_BYTES = 128
 
 # Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).

@@ -214,6 +214,13 @@ class PageRankGraph:
         """pr_set_option(PR_OPT_HOT_RESERVE): CUs per XCD the heavy SpMV kernel leaves free."""
         check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_HOT_RESERVE, int(cus_per_xcd)))
 
+    def set_exchange_ipc(self, on: bool) -> None:
+        """pr_set_option(PR_OPT_XCHG_IPC): RCCL path on one node -- every rank pulls the runs it reads
+        out of its peers' IPC-mapped send buffers with the copy engines (True) or RCCL send/recv
+        (False, the default).  Collective: every rank calls it; the first enable maps the peers'
+        buffers and raises on every rank if any rank cannot."""
+        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_IPC, 1 if on else 0))
+
     # -- multi-process -------------------------------------------------------------------------
     def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:
         buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES).from_buffer_copy(uid)

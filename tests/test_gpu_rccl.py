@@ -48,6 +48,17 @@ def _run(world, extra, scale=20, timeout=280, launcher=True, steps=6, warmup=2):
     return line
 
 
+def _check_ipc(line):
+    """The CU-free transport (PR_OPT_XCHG_IPC): its set-up succeeded on every rank, the calibration
+    timed it unchunked and chunked, and its ranks are bitwise the RCCL transport's (same runs, same
+    gather-space positions, only the mover differs) and within the oracle bar."""
+    ab, par = line["exchange_overlap_ab"], line["parity"]
+    assert "ipc_error" not in ab, ab.get("ipc_error")
+    assert ab["ipc_unchunked_ms_per_step"] > 0 and ab["ipc_chunked_ms_per_step"] > 0
+    assert par["ipc_bitwise_equal_rccl"] is True
+    assert par["max_rel_ipc_exchange"] <= RANK_TOL
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(320)
 @pytest.mark.parametrize(
@@ -71,8 +82,9 @@ def test_rccl_exchange_on_shared_device(world, extra):
         assert line["config"]["exchange_doubles_per_iter_rank0"] > 0
         ab = line["exchange_overlap_ab"]
         assert ab is not None and ab["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1",
-                                                   "chunked_reserve2")
+                                                   "chunked_reserve2", "ipc_unchunked", "ipc_chunked")
         assert par["max_rel_overlapped_exchange"] <= RANK_TOL
+        _check_ipc(line)
 
 
 @pytest.mark.gpu
@@ -100,4 +112,5 @@ def test_rccl_default_policy_at_baseline_size():
     par = line["parity"]
     assert par["every_row_owned_once"] is True
     assert par["max_rel"] <= RANK_TOL and par["max_rel_overlapped_exchange"] <= RANK_TOL
+    _check_ipc(line)
     assert line["roofline"]["classes"] == 64 and line["config"]["code_bits"] in (20, 24)
