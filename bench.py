@@ -439,11 +439,26 @@ def main() -> int:
             overlap["ipc_error"] = str(e)
             log(f"IPC exchange unavailable: {e}")
         for name, chunked, reserve, ipc in modes:
-            if ipc_ok:
-                g.set_exchange_ipc(ipc)
-            g.set_exchange_chunks(chunked)
-            g.set_hot_reserve(reserve)
-            ms = cal_steps(k_cal)
+            if ipc and not ipc_ok:
+                continue
+            try:
+                if ipc_ok:
+                    g.set_exchange_ipc(ipc)
+                g.set_exchange_chunks(chunked)
+                g.set_hot_reserve(reserve)
+                ms = cal_steps(k_cal)
+            except Exception as e:  # an IPC trial that fails drops the IPC modes, never the run
+                if not ipc:
+                    raise
+                overlap["ipc_error"] = f"{name}: {e}"
+                log(f"IPC exchange trial failed: {e}")
+                ipc_ok = False
+                try:
+                    g.set_exchange_ipc(False)
+                except Exception as e2:
+                    log(f"switching back to RCCL failed: {e2}")
+                    raise
+                continue
             overlap[f"{name}_ms_per_step"] = ms
             if best is None or ms < best[0]:
                 best = (ms, (name, chunked, reserve, ipc))
