@@ -40,6 +40,7 @@
 #include <thread>
 #include <vector>
 
+#include "pagerank_hip.h"
 #include "pr_graph.h"
 
 namespace pr {
@@ -369,25 +370,28 @@ int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   return PR_OK;
 }
 
-// Destroy: the peers may still be copying out of this rank's send buffers; wait (bounded) for the
-// copies of every exchange this rank published, then unmap everything.
+// Destroy: the peers may still be copying out of this rank's send buffers; wait for the copies of
+// every exchange this rank published, then unmap everything.  Host polls only, each bounded: a peer
+// that died mid-run must not hang this process's teardown.
 void ipc_destroy(pr_graph *g) {
   IpcState *s = g->ipc;
   if (!s) return;
   g->ipc = nullptr;
   g->x_ipc = false;
-  bool waited = false;
+  const std::string err = pr_last_error();  // the bounded waits below must not replace a real error
   for (int q = 0; q < s->P; ++q) {
     if (q == s->self || !s->peer[q]) continue;
     for (int b = 0; b < 2; ++b) {
       const int64_t k = s->mine->sent[b].load(std::memory_order_acquire);
       if (k <= 0) continue;
-      if (spin_until(s->peer[q]->copied[b], k, "copied", q, 10.0) != PR_OK) continue;  // peer gone: nothing to order
-      (void)hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + b], 0);
-      waited = true;
+      if (spin_until(s->peer[q]->copied[b], k, "copied", q, 10.0) != PR_OK) break;  // peer gone
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hipEventQuery(s->peer_copied[2 * q + b]) == hipErrorNotReady &&
+             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 10.0)
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
   }
-  if (waited) (void)hipStreamSynchronize(g->stream);
+  set_error(err);
   free_state(s);
 }
 
