@@ -110,7 +110,10 @@ constexpr int64_t kSplitMinSliceBytes = 4ll << 20;
 // Grouped epilogue (k_epilogue_grp): a wave takes kEpiGroup consecutive 64-row blocks and stages
 // their partial sums in an LDS window of kEpiWin slots, class runs a few at a time.
 constexpr int kEpiGroup = 8;
-constexpr int kEpiWin = 1024;  // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
+#ifndef PR_EPI_WIN
+#define PR_EPI_WIN 1024
+#endif
+constexpr int kEpiWin = PR_EPI_WIN;  // 8 KiB per wave; >= 64 * kEpiGroup + 2 (one class run always fits)
 constexpr int kEpiThreads = 256;  // 4 waves, 32.1 KiB of LDS: four workgroups per CU
 // narrow grouped epilogue: one-wave workgroups (8.2 KiB of LDS each), so a wave that finishes a
 // cheap group frees its window at once -- chosen when a graph has many walking (sparse) groups

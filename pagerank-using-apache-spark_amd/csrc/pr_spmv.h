@@ -833,6 +833,9 @@ struct EpiArgs {
 #ifndef PR_EPI_DMA_AUX
 #define PR_EPI_DMA_AUX 0
 #endif
+#ifndef PR_EPI_LATE_ROW
+#define PR_EPI_LATE_ROW 0  // 1: k_epilogue_grp loads rowinfo / r after the class loop (A/B builds)
+#endif
 
 // One group gi (kEpiGroup consecutive 64-row blocks) of the grouped epilogue, by one wave with its
 // LDS window win (kEpiWin slots + the zero slot win[kEpiWin]).  The group's dangling and L1
@@ -867,8 +870,10 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     } else {
       mw[0][g] = ok ? static_cast<const uint32_t *>(a.rmask)[L] : 0u;
     }
+#if !PR_EPI_LATE_ROW
     info[g] = ok ? a.rowinfo[L] : kRowHole;
     rold[g] = ok ? a.r[L] : 0.0;
+#endif
     S[g] = 0.0;
   }
   // lane x holds class x's run [cs, ce) (and class 64 + x's in cs1/ce1 at C = 128), read back
@@ -985,6 +990,16 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
       x = xe;
     }
   }
+#if PR_EPI_LATE_ROW
+  // the row data is loaded after the sums (fewer live registers through the class loop)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int64_t L = (b0 + g) * kWave + lane;
+    const bool ok = g < nb;
+    info[g] = ok ? a.rowinfo[L] : kRowHole;
+    rold[g] = ok ? a.r[L] : 0.0;
+  }
+#endif
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t L = (b0 + g) * kWave + lane;
@@ -1025,8 +1040,16 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
 
 //
 // Groups [g_lo, g_hi) of the pass (all of them in the product).
+#ifndef PR_EPI_WAVES
+#define PR_EPI_WAVES 0  // > 0: amdgpu_waves_per_eu floor of k_epilogue_grp (A/B builds)
+#endif
+#if PR_EPI_WAVES > 0
+#define PR_EPI_BOUNDS(NT) __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(PR_EPI_WAVES)))
+#else
+#define PR_EPI_BOUNDS(NT) __launch_bounds__(NT, 4)
+#endif
 template <int C, bool WALK, int NT>
-__global__ __launch_bounds__(NT, 4) void k_epilogue_grp(
+__global__ PR_EPI_BOUNDS(NT) void k_epilogue_grp(
     int64_t nblk, int64_t g_lo, int64_t g_hi, const double *__restrict__ partial, const void *__restrict__ rmask_v,
     const int32_t *__restrict__ cbase, const uint32_t *__restrict__ rowinfo, double *__restrict__ r,
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
