@@ -833,9 +833,6 @@ struct EpiArgs {
 #ifndef PR_EPI_DMA_AUX
 #define PR_EPI_DMA_AUX 0
 #endif
-#ifndef PR_EPI_DIAG_CONTIG
-#define PR_EPI_DIAG_CONTIG 0  // diagnostic builds only: see epi_group
-#endif
 #ifndef PR_EPI_LATE_ROW
 #define PR_EPI_LATE_ROW 0  // 1: k_epilogue_grp loads rowinfo / r after the class loop (A/B builds)
 #endif
@@ -893,14 +890,6 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
     const int incl = wave_incl_scan_i32(n2);
     const int pre = incl - n2;
     const int roff = incl - n2 + (cs - sa);  // window position of the run's first slot
-#if PR_EPI_DIAG_CONTIG
-    // DIAGNOSTIC ONLY (wrong sums): the group's runs read as one contiguous region of the same size
-    // at the group's share of the slot array, to time the DMA of a group-major slot layout
-    const int64_t total = a.cbase[a.nblk * C + C - 1];
-    const int64_t ngrp = (a.nblk + G - 1) / G;
-    const int64_t T = __builtin_amdgcn_readlane(incl, C - 1);
-    const int64_t dbase = max((int64_t)0, min(gi * total / ngrp, total - T)) & ~(int64_t)1;
-#endif
     bool walked = false;
     if constexpr (WALK) {
       const int64_t eo = a.eoff[gi];
@@ -910,11 +899,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
         for (int y = 0; y < C; ++y) {
           const int n = __builtin_amdgcn_readlane(n2, y);
           if (n == 0) continue;
-#if PR_EPI_DIAG_CONTIG
-          const double *src = a.partial + dbase + __builtin_amdgcn_readlane(pre, y);
-#else
           const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
-#endif
           double *dst = win + __builtin_amdgcn_readlane(pre, y);
           for (int o = 0; o < n; o += 2 * kWave)
             if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, PR_EPI_DMA_AUX);
@@ -948,11 +933,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
       for (int y = x0; y < x1; ++y) {
         const int n = __builtin_amdgcn_readlane(n2, y);
         if (n == 0) continue;
-#if PR_EPI_DIAG_CONTIG
-        const double *src = a.partial + dbase + __builtin_amdgcn_readlane(pre, y);
-#else
         const double *src = a.partial + __builtin_amdgcn_readlane(sa, y);
-#endif
         double *dst = win + (__builtin_amdgcn_readlane(pre, y) - base);
         for (int o = 0; o < n; o += 2 * kWave)
           if (o + 2 * lane < n) __builtin_amdgcn_global_load_lds(src + o + 2 * lane, dst + o, 16, 0, PR_EPI_DMA_AUX);
