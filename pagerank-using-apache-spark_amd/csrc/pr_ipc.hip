@@ -7,7 +7,9 @@
 // its completion signals differ:
 //   memory   every rank's double-buffered send runs (x_sbuf) are mapped into every peer
 //            (hipIpcGetMemHandle / hipIpcOpenMemHandle); a receiver copies run q -> its gather space
-//            with hipMemcpyDeviceToDeviceNoCU on its xstream, chunk by chunk (x_ev[c] as before).
+//            with hipMemcpyDeviceToDeviceNoCU on a copy stream of its own per peer (the peers' runs
+//            move at once, over their own links), chunk by chunk; the transfer stream (xstream)
+//            joins every peer's chunk c before it records x_ev[c], as the RCCL exchange does.
 //   device   two interprocess events per buffer b and rank: `sent[b]` (recorded on the owner's
 //            compute stream once the runs of b are written: fused epilogue + k_finalize, or k_pack)
 //            and `copied[b]` (recorded on the owner's xstream after its copies out of every peer's
@@ -83,6 +85,11 @@ struct IpcState {
   std::vector<int64_t> peer_soff_me;  // start of the peer's run for this rank
   hipEvent_t sent[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> peer_sent, peer_copied;  // [q * 2 + b]
+  // one copy stream per peer, so the runs of different peers move at once (on their own copy
+  // engines / xGMI links), and per (peer, chunk) the event the transfer stream joins on
+  std::vector<hipStream_t> cstream;
+  std::vector<hipEvent_t> cev;  // [q * nc + c]
+  int nc = 0;
   int64_t n[2] = {0, 0};      // exchanges of buffer b since the mode was (re)enabled
   int64_t freed[2] = {0, 0};  // exchange index of b whose send-run writes are already ordered
 };
@@ -114,6 +121,13 @@ IpcCounters *map_page(const char *name, bool create) {
 
 void free_state(IpcState *s) {
   if (!s) return;
+  for (hipStream_t st : s->cstream)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+  for (hipEvent_t e : s->cev)
+    if (e) (void)hipEventDestroy(e);
   for (size_t q = 0; q < s->peer_sbuf.size(); ++q)
     if (s->peer_sbuf[q]) (void)hipIpcCloseMemHandle(s->peer_sbuf[q]);
   for (hipEvent_t e : s->peer_sent)
@@ -183,6 +197,9 @@ int ipc_setup(pr_graph *g) {
   s->peer_soff_me.assign(P, 0);
   s->peer_sent.assign(2 * (size_t)P, nullptr);
   s->peer_copied.assign(2 * (size_t)P, nullptr);
+  s->cstream.assign(P, nullptr);
+  s->nc = g->n_xc;
+  s->cev.assign((size_t)P * s->nc, nullptr);
   std::string why;
   IpcRecord rec;
   std::memset(&rec, 0, sizeof(rec));
@@ -261,6 +278,18 @@ int ipc_setup(pr_graph *g) {
         why = "hipIpcOpenEventHandle failed";
       }
     }
+    if (ok && hipStreamCreateWithFlags(&s->cstream[q], hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      s->cstream[q] = nullptr;
+      ok = 0;
+      why = "hipStreamCreate failed";
+    }
+    for (int c = 0; c < s->nc && ok; ++c)
+      if (hipEventCreateWithFlags(&s->cev[(size_t)q * s->nc + c], hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        ok = 0;
+        why = "hipEventCreate failed";
+      }
     s->peer_stride[q] = r.stride;
     s->peer_soff_me[q] = r.soff[self];
     // the peer's run for this rank must be exactly what this rank receives from it
@@ -341,14 +370,18 @@ int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
   PR_HIP(hipEventRecord(s->sent[buf], g->stream));
   s->mine->sent[buf].store(k, std::memory_order_release);
-  PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));  // this rank's pass no longer reads cbuf[buf]
+  PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
+  if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
+  // per peer: its copy stream waits until this rank's pass no longer reads cbuf[buf] and the
+  // peer's runs of buf are written
   for (int q = 0; q < s->P; ++q) {
     if (q == s->self) continue;
+    PR_HIP(hipStreamWaitEvent(s->cstream[q], g->x_pack_ev, 0));
     PR_TRY(spin_until(s->peer[q]->sent[buf], k, "sent", q));
-    PR_HIP(hipStreamWaitEvent(g->xstream, s->peer_sent[2 * q + buf], 0));
+    PR_HIP(hipStreamWaitEvent(s->cstream[q], s->peer_sent[2 * q + buf], 0));
   }
-  if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
   const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
+  if (nc != s->nc) return fail(PR_ERR_STATE, "IPC exchange: chunk count changed");
   double *base = g->cbuf[buf].as<double>();
   for (int c = 0; c < steps; ++c) {
     const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;
@@ -359,7 +392,10 @@ int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
       const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(buf & 1) * s->peer_stride[q] +
                           s->peer_soff_me[q] + r0;
       PR_HIP(hipMemcpyAsync(base + g->S_pad + g->x_roff[q] + r0, src, sizeof(double) * (size_t)(r1 - r0),
-                            hipMemcpyDeviceToDeviceNoCU, g->xstream));
+                            hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
+      hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
+      PR_HIP(hipEventRecord(e, s->cstream[q]));
+      PR_HIP(hipStreamWaitEvent(g->xstream, e, 0));  // chunk c of every peer -> x_ev[c]
     }
     PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
   }
