@@ -44,6 +44,7 @@
 
 #include "pagerank_hip.h"
 #include "pr_graph.h"
+#include "pr_ipc_protocol.h"
 
 namespace pr {
 
@@ -75,6 +76,8 @@ struct IpcRecord {
 
 }  // namespace
 
+struct HipIpcOps;
+
 struct IpcState {
   int P = 0, self = 0;
   char page[64] = {0};
@@ -90,8 +93,7 @@ struct IpcState {
   std::vector<hipStream_t> cstream;
   std::vector<hipEvent_t> cev;  // [q * nc + c]
   int nc = 0;
-  int64_t n[2] = {0, 0};      // exchanges of buffer b since the mode was (re)enabled
-  int64_t freed[2] = {0, 0};  // exchange index of b whose send-run writes are already ordered
+  IpcProtocol<HipIpcOps> proto;  // the host-side ordering (pr_ipc_protocol.h)
 };
 
 namespace {
@@ -191,6 +193,8 @@ int ipc_setup(pr_graph *g) {
   if (!s) return fail(PR_ERR_OOM, "host allocation failed");
   s->P = P;
   s->self = self;
+  s->proto.P = P;
+  s->proto.self = self;
   s->peer.assign(P, nullptr);
   s->peer_sbuf.assign(P, nullptr);
   s->peer_stride.assign(P, 0);
@@ -332,75 +336,92 @@ int set_exchange_ipc(pr_graph *g, bool on) {
     for (int b = 0; b < 2; ++b) {
       s->mine->sent[b].store(0, std::memory_order_release);
       s->mine->copied[b].store(0, std::memory_order_release);
-      s->n[b] = s->freed[b] = 0;
     }
+    s->proto.reset();
   }
   PR_TRY(comm_barrier(g, &one));
   g->x_ipc = on;
   return PR_OK;
 }
 
+// The HIP side of the protocol's steps: interprocess events, the counter pages, the copy streams.
+struct HipIpcOps {
+  pr_graph *g;
+  IpcState *s;
+  hipEvent_t ev_a;  // timing: recorded on the transfer stream before the copies (may be null)
+
+  hipEvent_t peer_event(int q, int kind, int b) const {
+    return kind == kIpcSent ? s->peer_sent[2 * q + b] : s->peer_copied[2 * q + b];
+  }
+  int spin(int q, int kind, int b, int64_t v) {
+    const std::atomic<int64_t> &c = kind == kIpcSent ? s->peer[q]->sent[b] : s->peer[q]->copied[b];
+    return spin_until(c, v, kind == kIpcSent ? "sent" : "copied", q);
+  }
+  int wait_compute(int q, int kind, int b, int64_t) {
+    PR_HIP(hipStreamWaitEvent(g->stream, peer_event(q, kind, b), 0));
+    return PR_OK;
+  }
+  int wait_copy(int q, int kind, int b, int64_t) {
+    PR_HIP(hipStreamWaitEvent(s->cstream[q], peer_event(q, kind, b), 0));
+    return PR_OK;
+  }
+  int record(int kind, int b, int64_t k) {
+    if (kind == kIpcSent) {  // the runs of b are written: after the pass (+ pack) on the compute stream
+      PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
+      PR_HIP(hipEventRecord(s->sent[b], g->stream));
+      s->mine->sent[b].store(k, std::memory_order_release);
+    } else {  // the transfer stream has joined every copy of b
+      PR_HIP(hipEventRecord(s->copied[b], g->xstream));
+      s->mine->copied[b].store(k, std::memory_order_release);
+    }
+    return PR_OK;
+  }
+  int pack(int b) { return exchange_pack(g, b); }
+  int fail(const char *msg) { return pr::fail(PR_ERR_STATE, msg); }
+
+  // every copy stream waits until this rank's pass no longer reads cbuf[b]; then per chunk the
+  // copies of every peer, each joined by the transfer stream before it records x_ev[c]
+  int copies(int b) {
+    PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
+    if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
+    for (int q = 0; q < s->P; ++q)
+      if (q != s->self) PR_HIP(hipStreamWaitEvent(s->cstream[q], g->x_pack_ev, 0));
+    const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
+    if (nc != s->nc) return fail("IPC exchange: chunk count changed");
+    double *base = g->cbuf[b].as<double>();
+    for (int c = 0; c < steps; ++c) {
+      const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;
+      for (int q = 0; q < s->P; ++q) {
+        if (q == s->self) continue;
+        const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
+        if (r1 <= r0) continue;
+        const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(b & 1) * s->peer_stride[q] +
+                            s->peer_soff_me[q] + r0;
+        PR_HIP(hipMemcpyAsync(base + g->S_pad + g->x_roff[q] + r0, src, sizeof(double) * (size_t)(r1 - r0),
+                              hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
+        hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
+        PR_HIP(hipEventRecord(e, s->cstream[q]));
+        PR_HIP(hipStreamWaitEvent(g->xstream, e, 0));  // chunk c of every peer -> x_ev[c]
+      }
+      PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
+    }
+    return PR_OK;
+  }
+};
+
 // Before the compute stream writes the send runs of `buf` for the next exchange: order the writes
 // after every peer's copies of the previous exchange of `buf`.
 int ipc_send_runs_free(pr_graph *g, int buf) {
   if (!g->x_ipc) return PR_OK;
-  IpcState *s = g->ipc;
-  const int64_t k = s->n[buf] + 1;  // the exchange these writes belong to
-  if (s->freed[buf] >= k) return PR_OK;
-  if (k > 1) {
-    for (int q = 0; q < s->P; ++q) {
-      if (q == s->self) continue;
-      PR_TRY(spin_until(s->peer[q]->copied[buf], k - 1, "copied", q));
-      PR_HIP(hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + buf], 0));
-    }
-  }
-  s->freed[buf] = k;
-  return PR_OK;
+  HipIpcOps o{g, g->ipc, nullptr};
+  return g->ipc->proto.send_runs_free(o, buf);
 }
 
 int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
-  IpcState *s = g->ipc;
-  if (g->x_packed != buf) {
-    PR_TRY(ipc_send_runs_free(g, buf));
-    PR_TRY(exchange_pack(g, buf));
-  }
+  HipIpcOps o{g, g->ipc, ev_a};
+  const bool packed = g->x_packed == buf;
   g->x_packed = -1;
-  const int64_t k = ++s->n[buf];
-  if (s->freed[buf] < k) return fail(PR_ERR_STATE, "IPC exchange: send runs written without the reuse wait");
-  PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
-  PR_HIP(hipEventRecord(s->sent[buf], g->stream));
-  s->mine->sent[buf].store(k, std::memory_order_release);
-  PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
-  if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
-  // per peer: its copy stream waits until this rank's pass no longer reads cbuf[buf] and the
-  // peer's runs of buf are written
-  for (int q = 0; q < s->P; ++q) {
-    if (q == s->self) continue;
-    PR_HIP(hipStreamWaitEvent(s->cstream[q], g->x_pack_ev, 0));
-    PR_TRY(spin_until(s->peer[q]->sent[buf], k, "sent", q));
-    PR_HIP(hipStreamWaitEvent(s->cstream[q], s->peer_sent[2 * q + buf], 0));
-  }
-  const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
-  if (nc != s->nc) return fail(PR_ERR_STATE, "IPC exchange: chunk count changed");
-  double *base = g->cbuf[buf].as<double>();
-  for (int c = 0; c < steps; ++c) {
-    const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;
-    for (int q = 0; q < s->P; ++q) {
-      if (q == s->self) continue;
-      const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
-      if (r1 <= r0) continue;
-      const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(buf & 1) * s->peer_stride[q] +
-                          s->peer_soff_me[q] + r0;
-      PR_HIP(hipMemcpyAsync(base + g->S_pad + g->x_roff[q] + r0, src, sizeof(double) * (size_t)(r1 - r0),
-                            hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
-      hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
-      PR_HIP(hipEventRecord(e, s->cstream[q]));
-      PR_HIP(hipStreamWaitEvent(g->xstream, e, 0));  // chunk c of every peer -> x_ev[c]
-    }
-    PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
-  }
-  PR_HIP(hipEventRecord(s->copied[buf], g->xstream));
-  s->mine->copied[buf].store(k, std::memory_order_release);
+  PR_TRY(g->ipc->proto.exchange(o, buf, packed));
   if (ev_b) PR_HIP(hipEventRecord(ev_b, g->xstream));
   g->x_pending = true;
   return PR_OK;

@@ -1,0 +1,155 @@
+// CPU model checker of the IPC exchange's host-side ordering (csrc/pr_ipc_protocol.h), the same
+// template the library runs (csrc/pr_ipc.hip).  One thread per rank runs a seeded sequence of
+// resets and iterations -- the same sequence on every rank, as the library requires -- with random
+// delays; interprocess events are modelled as "the number of records enqueued so far" per (rank,
+// kind, buffer), and the record counters as atomics.  Every stream wait checks that the latest
+// record of the peer's event at that moment is exactly the record the protocol means (so the
+// device wait would bind to it), and the run ends without deadlock.  Used by
+// tests/test_ipc_protocol_cpu.py through ipc_model_run().
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pr_ipc_protocol.h"
+
+namespace {
+
+struct World {
+  int P;
+  // per (rank, kind, buffer): records enqueued ("latest record") and the published counter
+  std::vector<std::atomic<int64_t>> enq, pub;
+  std::mutex mu;
+  std::string err;
+  std::atomic<bool> failed{false};
+  std::atomic<int64_t> waits{0};
+  explicit World(int p) : P(p), enq(4 * (size_t)p), pub(4 * (size_t)p) {
+    for (auto &a : enq) a.store(0);
+    for (auto &a : pub) a.store(0);
+  }
+  size_t ix(int r, int kind, int b) const { return (size_t)r * 4 + (size_t)kind * 2 + (size_t)b; }
+  int fail(const std::string &m) {
+    std::lock_guard<std::mutex> g(mu);
+    if (err.empty()) err = m;
+    failed.store(true);
+    return -1;
+  }
+};
+
+struct ModelOps {
+  World *w;
+  int self;
+  std::mt19937_64 rng;
+  int max_delay_us;
+  bool broken;  // checker self-test: no host spin before the sent waits
+
+  void delay() {
+    if (max_delay_us <= 0) return;
+    const int d = (int)(rng() % (uint64_t)(max_delay_us + 1));
+    if (d > 0) std::this_thread::sleep_for(std::chrono::microseconds(d));
+    else std::this_thread::yield();
+  }
+  int spin(int q, int kind, int b, int64_t v) {
+    if (broken && kind == pr::kIpcSent) {
+      delay();
+      return 0;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    while (w->pub[w->ix(q, kind, b)].load(std::memory_order_acquire) < v) {
+      if (w->failed.load()) return -1;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(20))
+        return w->fail("deadlock: rank " + std::to_string(self) + " never saw record " + std::to_string(v) +
+                       " of rank " + std::to_string(q));
+      std::this_thread::yield();
+    }
+    delay();
+    return 0;
+  }
+  int wait_any(int q, int kind, int b, int64_t v) {
+    const int64_t latest = w->enq[w->ix(q, kind, b)].load(std::memory_order_acquire);
+    w->waits.fetch_add(1);
+    if (latest != v)
+      return w->fail("rank " + std::to_string(self) + " waits on rank " + std::to_string(q) + "'s " +
+                     (kind == pr::kIpcSent ? "sent" : "copied") + "[" + std::to_string(b) + "] meaning record " +
+                     std::to_string(v) + " but its latest record is " + std::to_string(latest));
+    delay();
+    return 0;
+  }
+  int wait_compute(int q, int kind, int b, int64_t v) { return wait_any(q, kind, b, v); }
+  int wait_copy(int q, int kind, int b, int64_t v) { return wait_any(q, kind, b, v); }
+  int record(int kind, int b, int64_t k) {
+    const int64_t e = w->enq[w->ix(self, kind, b)].fetch_add(1) + 1;
+    if (e != k) return w->fail("rank " + std::to_string(self) + " enqueued record " + std::to_string(e) + " as " + std::to_string(k));
+    delay();
+    w->pub[w->ix(self, kind, b)].store(k, std::memory_order_release);
+    delay();
+    return 0;
+  }
+  int pack(int) {
+    delay();
+    return 0;
+  }
+  int copies(int) {
+    delay();
+    return 0;
+  }
+  int fail(const char *m) { return w->fail(m); }
+};
+
+}  // namespace
+
+extern "C" {
+
+// P ranks run n_ops steps each (seeded: 0 = reset, which writes and exchanges buffer 0 with the
+// pack kernel; otherwise an iteration, whose pass writes the runs of the other buffer, packed or
+// not); returns the number of stream waits checked, or -1 with the first violation in err.
+// max_delay_us < 0: the checker's self-test -- the same run with the sent spins left out.
+int64_t ipc_model_run(int P, int n_ops, uint64_t seed, int max_delay_us, char *err, int errlen) {
+  if (P < 2 || P > 64 || n_ops < 0) return -1;
+  std::mt19937_64 ops_rng(seed);
+  std::vector<int> ops((size_t)n_ops);
+  for (auto &o : ops) o = (int)(ops_rng() % 8);  // 0: reset, 1..7: iterations (1: unfused pack)
+  World w(P);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; ++r)
+    th.emplace_back([&, r]() {
+      ModelOps o{&w, r, std::mt19937_64(seed * 1315423911ull + (uint64_t)r + 1), max_delay_us < 0 ? -max_delay_us : max_delay_us,
+                 max_delay_us < 0};
+      pr::IpcProtocol<ModelOps> proto;
+      proto.P = P;
+      proto.self = r;
+      int cur = 0;
+      for (int op : ops) {
+        if (w.failed.load()) return;
+        int rv;
+        if (op == 0) {  // pr_reset: k_finalize writes the slots of buffer 0's runs, then exchange(0)
+          cur = 0;
+          rv = proto.send_runs_free(o, 0);
+          if (rv == 0) rv = proto.exchange(o, 0, false);
+        } else {  // an iteration: the pass writes the runs of `out` (fused) unless op == 1
+          const int out = cur ^ 1;
+          rv = proto.send_runs_free(o, out);
+          if (rv == 0) rv = proto.exchange(o, out, op != 1);
+          cur = out;
+        }
+        if (rv != 0) {
+          w.fail("rank " + std::to_string(r) + ": protocol step failed");
+          return;
+        }
+      }
+    });
+  for (auto &t : th) t.join();
+  if (w.failed.load()) {
+    if (err && errlen > 0) std::snprintf(err, (size_t)errlen, "%s", w.err.c_str());
+    return -1;
+  }
+  return w.waits.load();
+}
+
+}  // extern "C"

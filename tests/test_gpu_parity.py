@@ -537,6 +537,24 @@ def test_hot_reserve_bitwise(hip, oracle_c):
     assert max_rel(out["0"], ref["ranks"]) <= RANK_TOL
 
 
+def test_exchange_ipc_option_checks(hip):
+    """PR_OPT_XCHG_IPC (the CU-free RCCL-path transport) needs an attached communicator: a single
+    graph refuses it with PR_ERR_STATE and keeps working; values other than 0 / 1 are PR_ERR_INVALID;
+    switching it off when it is off is a no-op."""
+    from sparky_hip import _lib
+
+    rng = np.random.default_rng(5)
+    V = 4000
+    src, dst = random_edges(rng, V, 40000, hub_frac=0.02)
+    with hip.PageRankGraph(V, src, dst, keep_canonical=False) as g:
+        with pytest.raises(Exception, match="communicator"):
+            g.set_exchange_ipc(True)
+        g.set_exchange_ipc(False)
+        assert _lib.load().pr_set_option(g._h, _lib.PR_OPT_XCHG_IPC, 2) == _lib.PR_ERR_INVALID
+        r, _ = g.run(3)
+        assert np.isfinite(r).all()
+
+
 @pytest.mark.parametrize("classes", ["64", "32", "16"])
 def test_epilogue_row_walk_bitwise(hip, oracle_c, classes):
     """k_epilogue_grp walks the rows of sparse groups over their own slots (PR_BOPT_EPI_WALK=1,

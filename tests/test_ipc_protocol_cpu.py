@@ -1,0 +1,56 @@
+"""CPU model check of the IPC exchange's host-side ordering (PR_OPT_XCHG_IPC).
+
+The library's CU-free transport (csrc/pr_ipc.hip) orders its copy-engine pulls with interprocess
+events, and a wait on such an event binds to the latest record enqueued when the wait is enqueued.
+Its hosts therefore publish record counts and spin before every wait (csrc/pr_ipc_protocol.h).  The
+same protocol template runs here in host/ipc_model.cpp with one thread per rank, random delays
+between every step and events modelled as "records enqueued so far": every wait must find exactly
+the record it means as the peer's latest (never an older one -- the device would not wait for the
+data -- nor a newer one -- it would wait for the wrong iteration), and no rank may deadlock, over
+seeded sequences of resets, fused-pack and pack-kernel iterations (buffer reuse every other
+iteration; a reset exchanges buffer 0 again).  The GPU tests (tests/test_gpu_rccl.py) run the
+transport itself and check its ranks bitwise against RCCL's.
+"""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "pagerank-using-apache-spark_amd", "build", "libpr_ipc_model.so")
+
+
+@pytest.fixture(scope="module")
+def model():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host")], check=True)
+    lib = ctypes.CDLL(LIB)
+    lib.ipc_model_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p,
+                                  ctypes.c_int]
+    lib.ipc_model_run.restype = ctypes.c_int64
+    return lib
+
+
+def _run(model, P, n_ops, seed, delay_us):
+    err = ctypes.create_string_buffer(512)
+    waits = model.ipc_model_run(P, n_ops, seed, delay_us, err, len(err))
+    assert waits >= 0, err.value.decode()
+    return waits
+
+
+@pytest.mark.parametrize("P,n_ops,seed,delay_us", [(2, 400, 1, 0), (2, 200, 2, 30), (3, 200, 3, 20), (4, 150, 4, 20),
+                                                   (8, 80, 5, 10), (8, 150, 6, 0)])
+def test_every_wait_binds_to_the_record_it_means(model, P, n_ops, seed, delay_us):
+    waits = _run(model, P, n_ops, seed, delay_us)
+    # every exchange waits on each peer's sent record, and every reuse of a buffer on each peer's
+    # copied record of its previous exchange
+    assert waits >= n_ops * (P - 1)
+
+
+def test_the_model_catches_a_broken_order(model):
+    """Sanity of the checker itself: a protocol that skips the host spin before the sent wait must be
+    caught -- with delays, some rank enqueues its wait before the peer has recorded that exchange.
+    (ipc_model_run with a negative delay runs that broken variant.)"""
+    err = ctypes.create_string_buffer(512)
+    caught = any(model.ipc_model_run(4, 200, s, -30, err, len(err)) < 0 for s in range(1, 6))
+    assert caught and b"latest record" in err.value
