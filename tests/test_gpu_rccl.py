@@ -67,8 +67,9 @@ def _check_ipc(line):
         (2, ["--build-option", "classes=16"]),  # sparse runs; calibration of unchunked / chunked (2 chunks)
         (3, ["--build-option", "classes=32"]),  # odd rank count, 4 chunks per run
         (2, ["--build-option", "exchange_allgather=1"]),  # whole-slice ncclAllGather (A/B reference)
+        (2, ["--graph", "lj"]),  # BASELINE configs[1] (LiveJournal shape) at its policy, RCCL and IPC
     ],
-    ids=["p2-c16-sparse", "p3-c32-sparse", "p2-allgather"],
+    ids=["p2-c16-sparse", "p3-c32-sparse", "p2-allgather", "p2-lj"],
 )
 def test_rccl_exchange_on_shared_device(world, extra):
     line = _run(world, extra)
