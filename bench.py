@@ -402,7 +402,7 @@ def main() -> int:
     # left to the transfer kernels, which cannot share a CU with k_spmv_hot (pr_set_option,
     # collective) -- and the fastest one (the max over ranks, so every rank picks the same) is the
     # configuration timed below; every mode's calibration time is reported (exchange_overlap_ab)
-    # and the parity leg checks both exchange modes
+    # and the parity leg checks the RCCL modes and the IPC transport (bitwise against RCCL)
     overlap = None
     mode = ("unchunked", False, 0, False)
     ipc_ok = False
