@@ -223,12 +223,151 @@ def oracle_leg(g, V: int, iters: int, pick_threads: bool, raw=None):
     return res, threads, desc, csr.n_edges, same
 
 
+RANK_TOL = 1e-9  # north_star: ranks within 1e-9 max relative error of the reference's
+
+
+def parity_failures(parity) -> list:
+    """Every parity field of the line that fails its bar (empty: all pass, or no parity leg ran).
+    The line's value is nulled when any fails."""
+    if parity is None:
+        return []
+    bad = []
+    for k, v in parity.items():
+        if k.startswith("max_rel") and v is not None and not (v <= RANK_TOL):
+            bad.append(f"{k} = {v:.3e} > {RANK_TOL:g}")
+        elif (k.endswith("bitwise_equal_rccl") or k in ("csr_bit_exact", "every_row_owned_once")) and v is False:
+            bad.append(f"{k} is false")
+    for name, rec in (parity.get("modes") or {}).items():
+        if not rec.get("bitwise_equal_rccl_unchunked", True):
+            bad.append(f"mode {name} not bitwise equal to RCCL unchunked")
+        if not (rec.get("max_rel", 0.0) <= RANK_TOL):
+            bad.append(f"mode {name} max_rel {rec['max_rel']:.3e}")
+    return bad
+
+
 def contract_error_line(world: int, steps: int, warmup: int, msg: str) -> dict:
     """The contract's JSON line for a run that measured nothing ("value": null, "error")."""
     return {"metric": METRIC, "value": None, "unit": "GTEPS", "n_gpus": world, "steps": steps, "warmup": warmup,
             "ms_per_step": None, "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded device-side generator; no dataset)", "config": {"workload": None},
             "roofline": None, "cpu_baseline": None, "error": msg}
+
+
+EXCHANGE_MODES = [("unchunked", False, 0, False), ("chunked_reserve0", True, 0, False),
+                  ("chunked_reserve1", True, 1, False), ("chunked_reserve2", True, 2, False)]
+IPC_MODES = [("ipc_unchunked", False, 0, True), ("ipc_chunked", True, 0, True)]
+
+
+def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chunks: int, device: str = "cuda",
+                       k_chk: int = 3):
+    """N > 1: pick the exchange mode of the timed run.  Modes: whole runs after the pass (the
+    library default), overlapped with the next SpMV's phases with 0 / 1 / 2 CUs per XCD left to
+    the transfer kernels (which cannot share a CU with k_spmv_hot), and the CU-free IPC transport
+    unchunked / chunked (pr_set_option, collective).  A mode is a candidate only once k_chk of its
+    steps gave, on every rank, bitwise the ranks of the RCCL unchunked exchange (an
+    unverified transport is never timed).  Every outcome -- an exception on any rank, a mismatch --
+    is MIN-reduced over the ranks, so they all decide alike; a failed IPC trial switches every
+    rank back to RCCL together, and a failure of that switch ends the run (RuntimeError -> error
+    line).  The fastest candidate (max over ranks) wins.  Returns (report, mode, ipc_ok); mode =
+    (name, chunked, reserve, ipc), already applied."""
+    import numpy as np
+    import torch
+
+    def sync():
+        if device == "cuda":
+            torch.cuda.synchronize()
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def cal_steps(k):
+        g.reset()
+        g.step(warmup)
+        g.sync()
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        g.step(k)
+        g.sync()
+        sync()
+        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        dist.barrier()
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        return round(float(tc.item()) / max(k, 1) * 1e3, 4)
+
+    def local_after(k):
+        """this rank's rows after k iterations from a fresh reset in the current mode"""
+        g.reset()
+        g.step(k)
+        g.sync()
+        out = np.zeros(max(V, 1), np.float64)
+        g.ranks(out)
+        return out
+
+    overlap = {"calibration_steps": k_cal, "check_steps": k_chk, "chunks": chunks,
+               "library_default": "unchunked", "candidates_bitwise_checked": True}
+    g.set_exchange_chunks(False)
+    g.set_hot_reserve(0)
+    ref_local = local_after(k_chk)  # RCCL, whole runs: the library default
+    ipc_ok = False
+    try:  # the IPC set-up is collective and fails on every rank alike (agreed inside the library)
+        g.set_exchange_ipc(True)
+        g.set_exchange_ipc(False)
+        ipc_ok = True
+    except Exception as e:
+        overlap["ipc_error"] = str(e)
+        log(f"IPC exchange unavailable: {e}")
+    if not agree(ipc_ok) and ipc_ok:
+        raise RuntimeError("IPC set-up succeeded on this rank but not on every rank")
+    modes = EXCHANGE_MODES + (IPC_MODES if ipc_ok else [])
+    best, rejected = None, {}
+    for name, chunked, reserve, ipc in modes:
+        if ipc and not ipc_ok:
+            continue
+        err, same = None, False
+        try:
+            if ipc_ok:
+                g.set_exchange_ipc(ipc)
+            g.set_exchange_chunks(chunked)
+            g.set_hot_reserve(reserve)
+            same = name == "unchunked" or bool(np.array_equal(local_after(k_chk), ref_local))
+        except Exception as e:
+            err = f"{name}: {e}"
+            log(f"exchange mode trial failed on rank {rank}: {e}")
+        if not agree(err is None):
+            if not ipc:
+                raise RuntimeError(f"exchange mode {name} failed on a rank ({err or 'a peer'})")
+            overlap["ipc_error"] = err or f"{name}: failed on a peer"
+            ipc_ok = False
+            back = True
+            try:
+                g.set_exchange_ipc(False)
+            except Exception as e2:
+                log(f"switching back to RCCL failed: {e2}")
+                back = False
+            if not agree(back):
+                raise RuntimeError(f"IPC trial failed ({overlap['ipc_error']}) and the switch back to RCCL "
+                                   "failed on a rank")
+            continue
+        if not agree(same):  # bitwise on every rank, or not a candidate
+            rejected[name] = f"ranks after {k_chk} steps differ from the RCCL unchunked exchange's"
+            log(f"exchange mode {name} rejected: not bitwise equal to RCCL unchunked")
+            continue
+        ms = cal_steps(k_cal)
+        overlap[f"{name}_ms_per_step"] = ms
+        if best is None or ms < best[0]:
+            best = (ms, (name, chunked, reserve, ipc))
+    if rejected:
+        overlap["rejected"] = rejected
+    mode = best[1]
+    if ipc_ok:
+        g.set_exchange_ipc(mode[3])
+    g.set_exchange_chunks(mode[1])
+    g.set_hot_reserve(mode[2])
+    overlap["chosen"] = mode[0]
+    return overlap, mode, ipc_ok
 
 
 def launch_ranks(a) -> int:
@@ -400,74 +539,19 @@ def main() -> int:
     # N > 1: the exchange mode of the timed run is calibrated first -- whole runs after the pass
     # (the library default) or overlapped with the next SpMV's phases with 0 / 1 / 2 CUs per XCD
     # left to the transfer kernels, which cannot share a CU with k_spmv_hot (pr_set_option,
-    # collective) -- and the fastest one (the max over ranks, so every rank picks the same) is the
-    # configuration timed below; every mode's calibration time is reported (exchange_overlap_ab)
-    # and the parity leg checks the RCCL modes and the IPC transport (bitwise against RCCL)
+    # collective), and the CU-free IPC transport unchunked / chunked.  A mode is a candidate only
+    # once a few of its steps gave, on every rank, bitwise the ranks of the RCCL unchunked exchange
+    # (an unverified transport is never timed); every outcome -- an exception on any
+    # rank, a mismatch -- is MIN-reduced over the ranks so they all decide alike.  The fastest
+    # candidate (max over ranks) is the configuration timed below; the parity leg then checks that
+    # very configuration against the oracle (parity.timed_mode).
     overlap = None
     mode = ("unchunked", False, 0, False)
     ipc_ok = False
     if dist is not None and info.get("classes", 1) >= 16 and not a.no_overlap_ab:
-        def cal_steps(k):
-            g.reset()
-            g.step(a.warmup)
-            g.sync()
-            dist.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            g.step(k)
-            g.sync()
-            torch.cuda.synchronize()
-            tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-            dist.barrier()
-            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
-            return round(float(tc.item()) / max(k, 1) * 1e3, 4)
-
         wd.enter("calibration", limits["calibration"])
-        k_cal = max(5, a.steps // 2)
-        overlap = {"calibration_steps": k_cal, "chunks": info.get("classes", 1) // 8, "library_default": "unchunked"}
-        best = None
-        modes = [("unchunked", False, 0, False), ("chunked_reserve0", True, 0, False),
-                 ("chunked_reserve1", True, 1, False), ("chunked_reserve2", True, 2, False)]
-        # the CU-free transport (PR_OPT_XCHG_IPC): the copy engines pull the runs out of the peers'
-        # IPC-mapped send buffers; its set-up is collective and fails on every rank alike
-        try:
-            g.set_exchange_ipc(True)
-            g.set_exchange_ipc(False)
-            ipc_ok = True
-            modes += [("ipc_unchunked", False, 0, True), ("ipc_chunked", True, 0, True)]
-        except Exception as e:
-            overlap["ipc_error"] = str(e)
-            log(f"IPC exchange unavailable: {e}")
-        for name, chunked, reserve, ipc in modes:
-            if ipc and not ipc_ok:
-                continue
-            try:
-                if ipc_ok:
-                    g.set_exchange_ipc(ipc)
-                g.set_exchange_chunks(chunked)
-                g.set_hot_reserve(reserve)
-                ms = cal_steps(k_cal)
-            except Exception as e:  # an IPC trial that fails drops the IPC modes, never the run
-                if not ipc:
-                    raise
-                overlap["ipc_error"] = f"{name}: {e}"
-                log(f"IPC exchange trial failed: {e}")
-                ipc_ok = False
-                try:
-                    g.set_exchange_ipc(False)
-                except Exception as e2:
-                    log(f"switching back to RCCL failed: {e2}")
-                    raise
-                continue
-            overlap[f"{name}_ms_per_step"] = ms
-            if best is None or ms < best[0]:
-                best = (ms, (name, chunked, reserve, ipc))
-        mode = best[1]
-        if ipc_ok:
-            g.set_exchange_ipc(mode[3])
-        g.set_exchange_chunks(mode[1])
-        g.set_hot_reserve(mode[2])
-        overlap["chosen"] = mode[0]
+        overlap, mode, ipc_ok = calibrate_exchange(g, dist, V, rank, max(5, a.steps // 2), a.warmup,
+                                                   info.get("classes", 1) // 8)
         log(f"exchange mode calibration: {overlap}")
 
     wd.enter("timed", limits["timed"])
@@ -517,40 +601,60 @@ def main() -> int:
         K = a.parity_iters
 
         def gpu_ranks():
-            """K iterations from a fresh reset; every rank's rows summed on rank 0."""
+            """K iterations from a fresh reset in the current mode: (this rank's rows, every rank's rows
+            summed on rank 0, every row owned exactly once)."""
             g.reset()
             g.step(K)
             g.sync()
             mine = np.zeros(V, np.float64)
             g.ranks(mine)  # this rank's rows; the others stay 0
-            owned_once = True
+            merged, owned_once = mine, True
             if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
                 rt = torch.from_numpy(mine).cuda()
                 own = torch.from_numpy((mine != 0).astype(np.int32)).cuda()
                 dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
                 dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
                 if rank == 0:
-                    mine = rt.cpu().numpy()
+                    merged = rt.cpu().numpy()
                     owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
                 del rt, own
-            return mine, owned_once
+            return mine, merged, owned_once
 
-        g.set_hot_reserve(0)  # results do not depend on it (bitwise tested); every exchange mode
-        if ipc_ok:
-            g.set_exchange_ipc(False)
-        g.set_exchange_chunks(False)
-        mine, owned_once = gpu_ranks()
-        mine_chunked = mine_ipc = None
+        def set_mode(m):
+            if ipc_ok:
+                g.set_exchange_ipc(m[3])
+            g.set_exchange_chunks(m[1])
+            g.set_hot_reserve(m[2])
+
+        def all_ranks_equal(x, y) -> bool:
+            ok = bool(np.array_equal(x, y))
+            if dist is None:
+                return ok
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
+        # the RCCL unchunked exchange (the library default) is the reference every other mode must
+        # equal bit for bit on every rank; then the timed configuration itself (its chunking, hot
+        # reserve and transport), and every other transport setting the calibration could pick
+        ref_mode = ("unchunked", False, 0, False)
+        set_mode(ref_mode)
+        ref_local, mine, owned_once = gpu_ranks()
+        checked = {}  # name -> (merged ranks on rank 0, bitwise equal to the reference on every rank)
         if overlap is not None:
-            g.set_exchange_chunks(True)
-            mine_chunked, oc = gpu_ranks()
-            owned_once = owned_once and oc
-            if ipc_ok:  # the IPC transport (chunked) must give bitwise the RCCL transport's ranks
-                g.set_exchange_ipc(True)
-                mine_ipc, oc = gpu_ranks()
+            others = [mode] + [m for m in (("chunked_reserve0", True, 0, False), ("ipc_unchunked", False, 0, True),
+                                           ("ipc_chunked", True, 0, True))
+                               if m[0] != mode[0] and (ipc_ok or not m[3])]
+            for m in others:
+                if m[0] == ref_mode[0]:
+                    continue
+                set_mode(m)
+                loc, merged, oc = gpu_ranks()
                 owned_once = owned_once and oc
-                g.set_exchange_ipc(False)
-            g.set_exchange_chunks(False)
+                checked[m[0]] = (merged if rank == 0 else None, all_ranks_equal(loc, ref_local))
+                del loc
+            set_mode(ref_mode)
+        del ref_local
         if rank == 0:
             try:
                 res, threads, desc, e_csr, same = oracle_leg(g, V, K, pick_threads=True, raw=raw or None)
@@ -561,13 +665,30 @@ def main() -> int:
                                  else "oracle/pagerank_oracle.c on the exported canonical CSR"),
                           "csr_bit_exact": same,
                           "ranks_from": f"{world} rank(s)", "every_row_owned_once": owned_once}
-                if mine_chunked is not None:
-                    parity["max_rel_overlapped_exchange"] = float(np.max(np.abs(mine_chunked - ref) / ref))
-                    parity["max_rel"] = max(parity["max_rel"], parity["max_rel_overlapped_exchange"])
-                if mine_ipc is not None:
-                    parity["max_rel_ipc_exchange"] = float(np.max(np.abs(mine_ipc - ref) / ref))
-                    parity["ipc_bitwise_equal_rccl"] = bool(np.array_equal(mine_ipc, mine_chunked))
-                    parity["max_rel"] = max(parity["max_rel"], parity["max_rel_ipc_exchange"])
+                parity["timed_mode"] = mode[0] if world > 1 else None
+                if world > 1:
+                    parity["max_rel_timed_mode"] = parity["max_rel"]
+                    parity["timed_mode_bitwise_equal_rccl"] = True
+                per_mode = {}
+                for name, (merged, same_bits) in checked.items():
+                    mr = float(np.max(np.abs(merged - ref) / ref)) if V else 0.0
+                    per_mode[name] = {"max_rel": mr, "bitwise_equal_rccl_unchunked": same_bits}
+                    parity["max_rel"] = max(parity["max_rel"], mr)
+                    if name == mode[0]:
+                        parity["max_rel_timed_mode"] = mr
+                        parity["timed_mode_bitwise_equal_rccl"] = same_bits
+                if per_mode:
+                    parity["modes"] = per_mode
+                    if "chunked_reserve0" in per_mode:
+                        parity["max_rel_overlapped_exchange"] = per_mode["chunked_reserve0"]["max_rel"]
+                    for nm in ("ipc_unchunked", "ipc_chunked"):
+                        if nm in per_mode:
+                            parity[f"{nm}_bitwise_equal_rccl"] = per_mode[nm]["bitwise_equal_rccl_unchunked"]
+                    if "ipc_unchunked" in per_mode and "ipc_chunked" in per_mode:
+                        parity["ipc_bitwise_equal_rccl"] = (parity["ipc_unchunked_bitwise_equal_rccl"]
+                                                            and parity["ipc_chunked_bitwise_equal_rccl"])
+                        parity["max_rel_ipc_exchange"] = max(per_mode["ipc_unchunked"]["max_rel"],
+                                                             per_mode["ipc_chunked"]["max_rel"])
                 if world == 1 and K >= 2:
                     it_ms = res["iter_ms"][1:]
                     med = float(np.median(it_ms))
@@ -589,9 +710,12 @@ def main() -> int:
     wd.done()
 
     if rank == 0:
+        bad = parity_failures(parity)
+        if bad:
+            log("parity failed: " + "; ".join(bad))
         line = {
             "metric": METRIC,
-            "value": round(gteps, 3),
+            "value": None if bad else round(gteps, 3),
             "unit": "GTEPS",
             "n_gpus": world,
             "steps": a.steps,
@@ -646,11 +770,36 @@ def main() -> int:
             "parity": parity,
             "cpu_baseline": cpu,
         }
+        if bad:  # a number whose results differ from the oracle's is not a measurement
+            line["error"] = "parity failed: " + "; ".join(bad)
+            line["ms_per_step_unverified"] = line.pop("ms_per_step")
+            line["ms_per_step"] = None
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     return 0
 
 
+def main_guarded() -> int:
+    """main(), but an exception on rank 0 still prints the contract's line ("value": null, "error")."""
+    try:
+        return main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # noqa: B902 -- reported, then re-raised as a status
+        import traceback
+
+        traceback.print_exc()
+        if int(os.environ.get("RANK", "0")) == 0:
+            ap = argparse.ArgumentParser(add_help=False)
+            ap.add_argument("--steps", type=int, default=20)
+            ap.add_argument("--warmup", type=int, default=3)
+            ap.add_argument("--gpus", type=int, default=1)
+            k, _ = ap.parse_known_args()
+            world = int(os.environ.get("WORLD_SIZE", str(k.gpus)))
+            print(json.dumps(contract_error_line(world, k.steps, k.warmup, f"{type(e).__name__}: {e}")), flush=True)
+        return 1
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main_guarded())

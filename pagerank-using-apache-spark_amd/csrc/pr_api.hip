@@ -410,6 +410,7 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
     return fail(PR_ERR_INVALID, "rank/n_ranks must equal the graph's part/n_parts");
   if (g->comm) return fail(PR_ERR_STATE, "communicator already attached");
   DeviceGuard dg(g->device);
+  if (!g->comm_scratch.p) PR_TRY(g->comm_scratch.alloc(pr::kCommScratchBytes));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclResult_t rc = ncclCommInitRank(&g->comm, n_ranks, uid, rank);
@@ -511,6 +512,18 @@ int pr_group_sync(pr_graph *const *parts, int32_t n_parts) {
 void pr_graph_destroy(pr_graph *g) {
   if (!g) return;
   DeviceGuard dg(g->device);
+  if (g->ipc) {
+    // IPC transport: the compute stream may hold a wait on a peer's copied[] event and
+    // the transfer stream one on a peer's sent[] event; if that peer died they never fire.  Poll with
+    // a deadline instead of an unbounded synchronize; on expiry the handle and its device memory are
+    // leaked (freeing memory a wedged stream may still touch is worse), and the error says so.
+    const bool idle = pr::stream_idle_within(g->stream, 30.0) && pr::stream_idle_within(g->xstream, 30.0);
+    if (!idle) {
+      pr::set_error("pr_graph_destroy: a stream did not drain within 30 s (a peer of the IPC exchange died?); "
+                    "the handle is leaked");
+      return;
+    }
+  }
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   if (g->xstream) (void)hipStreamSynchronize(g->xstream);
   pr::ipc_destroy(g);  // after the peers' last copies out of this part's send runs

@@ -172,6 +172,10 @@ struct pr_graph {
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
   int comm_rank = 0, comm_size = 1;
+  // device scratch of the library's small collectives (the IPC set-up's record all-gather, the
+  // agreement all-reduces), allocated before the communicator: no rank can fail to take part in a
+  // collective for want of a buffer
+  pr::DevBuf comm_scratch;
   // single-process group (pr_group_*): the group performs the exchange by device copies
   bool grouped = false;
   hipEvent_t xev = nullptr;
@@ -180,6 +184,7 @@ struct pr_graph {
 };
 
 namespace pr {
+constexpr size_t kCommScratchBytes = 128 << 10;
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (after rmask/cbase)
@@ -214,6 +219,7 @@ int set_exchange_ipc(pr_graph *g, bool on);
 int ipc_send_runs_free(pr_graph *g, int buf);
 int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b);
 void ipc_destroy(pr_graph *g);
+bool stream_idle_within(hipStream_t s, double seconds);  // host poll of hipStreamQuery with a deadline
 hipEvent_t next_event(pr_graph *g);  // the next timing event of g's pool (nullptr: creation failed)
 int time_mark(pr_graph *g, hipStream_t s, int *index);  // records one on s; *index into ev_pool
 }  // namespace pr

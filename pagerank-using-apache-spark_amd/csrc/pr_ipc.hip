@@ -143,7 +143,7 @@ void free_state(IpcState *s) {
   for (IpcCounters *c : s->peer) unmap_page(c);
   if (s->mine) {
     unmap_page(s->mine);
-    shm_unlink(s->page);  // normally unlinked at set-up already
+    if (s->page[0]) shm_unlink(s->page);  // normally unlinked at set-up already
   }
   (void)hipGetLastError();
   delete s;
@@ -167,14 +167,15 @@ int spin_until(const std::atomic<int64_t> &c, int64_t v, const char *what, int p
   return PR_OK;
 }
 
-// every rank's streams are idle and every rank got here (tiny all-reduce on the compute stream)
+// every rank's streams are idle and every rank got here (tiny all-reduce on the compute stream,
+// through the scratch allocated with the communicator: no allocation can fail here on one rank only)
 int comm_barrier(pr_graph *g, int32_t *flag_inout) {
-  DevBuf d;
-  PR_TRY(d.alloc(sizeof(int32_t)));
-  PR_HIP(hipMemcpyAsync(d.p, flag_inout, sizeof(int32_t), hipMemcpyHostToDevice, g->stream));
-  const ncclResult_t rc = ncclAllReduce(d.p, d.p, 1, ncclInt32, ncclMin, g->comm, g->stream);
+  if (!g->comm_scratch.p) return fail(PR_ERR_STATE, "no communicator scratch (pr_graph_attach_comm)");
+  void *d = g->comm_scratch.p;
+  PR_HIP(hipMemcpyAsync(d, flag_inout, sizeof(int32_t), hipMemcpyHostToDevice, g->stream));
+  const ncclResult_t rc = ncclAllReduce(d, d, 1, ncclInt32, ncclMin, g->comm, g->stream);
   if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(rc));
-  PR_HIP(hipMemcpyAsync(flag_inout, d.p, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipMemcpyAsync(flag_inout, d, sizeof(int32_t), hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
   return PR_OK;
 }
@@ -186,11 +187,42 @@ int quiesce(pr_graph *g) {
   return PR_OK;
 }
 
-// collective: map every peer's send buffers, events and counter page
+// the IPC state of a set-up in progress: freed (events, mappings, the counter page and its name)
+// on every return that does not hand it to the graph
+struct IpcStateGuard {
+  IpcState *s;
+  ~IpcStateGuard() { free_state(s); }
+  IpcState *release() {
+    IpcState *t = s;
+    s = nullptr;
+    return t;
+  }
+};
+
+static_assert(sizeof(IpcRecord) * (kMaxParts + 1) <= kCommScratchBytes, "IPC records exceed the comm scratch");
+
+// collective: map every peer's send buffers, events and counter page.  Every local failure goes
+// through rec.ok, so every rank reaches the record all-gather and the agreement all-reduce whatever
+// failed where; only a failing collective itself returns early.
 int ipc_setup(pr_graph *g) {
   const int P = g->nparts, self = g->part;
-  IpcState *s = new (std::nothrow) IpcState();
-  if (!s) return fail(PR_ERR_OOM, "host allocation failed");
+  if (!g->comm_scratch.p) return fail(PR_ERR_STATE, "no communicator scratch (pr_graph_attach_comm)");
+  IpcState *s0 = new (std::nothrow) IpcState();
+  IpcStateGuard guard{s0};
+  std::string why;
+  IpcRecord rec;
+  std::memset(&rec, 0, sizeof(rec));
+  rec.ok = 1;
+  auto local = [&](bool cond, const char *what) {
+    if (!cond && rec.ok) {
+      rec.ok = 0;
+      why = what;
+    }
+    (void)hipGetLastError();
+  };
+  local(s0 != nullptr, "host allocation failed");
+  IpcState dummy;  // stands in for a failed allocation so the collectives below still run
+  IpcState *s = s0 ? s0 : &dummy;
   s->P = P;
   s->self = self;
   s->proto.P = P;
@@ -204,23 +236,14 @@ int ipc_setup(pr_graph *g) {
   s->cstream.assign(P, nullptr);
   s->nc = g->n_xc;
   s->cev.assign((size_t)P * s->nc, nullptr);
-  std::string why;
-  IpcRecord rec;
-  std::memset(&rec, 0, sizeof(rec));
-  rec.ok = 1;
-  auto local = [&](bool cond, const char *what) {
-    if (!cond && rec.ok) {
-      rec.ok = 0;
-      why = what;
-    }
-    (void)hipGetLastError();
-  };
-  std::snprintf(s->page, sizeof(s->page), "/pr_xipc_%d_%d_%llx", (int)getpid(), self,
-                (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
-  s->mine = map_page(s->page, true);
-  local(s->mine != nullptr, "shm_open of the counter page failed");
-  std::memcpy(rec.page, s->page, sizeof(rec.page));
-  local(hipIpcGetMemHandle(&rec.mem, g->x_sbuf.p) == hipSuccess, "hipIpcGetMemHandle failed");
+  if (rec.ok) {
+    std::snprintf(s->page, sizeof(s->page), "/pr_xipc_%d_%d_%llx", (int)getpid(), self,
+                  (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
+    s->mine = map_page(s->page, true);
+    local(s->mine != nullptr, "shm_open of the counter page failed");
+    std::memcpy(rec.page, s->page, sizeof(rec.page));
+  }
+  if (rec.ok) local(hipIpcGetMemHandle(&rec.mem, g->x_sbuf.p) == hipSuccess, "hipIpcGetMemHandle failed");
   for (int b = 0; b < 2 && rec.ok; ++b) {
     local(hipEventCreateWithFlags(&s->sent[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&s->copied[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
@@ -232,23 +255,15 @@ int ipc_setup(pr_graph *g) {
   }
   rec.stride = send_stride(g);
   for (int q = 0; q <= P; ++q) rec.soff[q] = g->x_soff[q];
-  // publish
+  // publish (the scratch holds P + 1 records: this rank's, then everyone's)
   std::vector<IpcRecord> all((size_t)P);
   {
-    DevBuf d;
     const size_t W = sizeof(IpcRecord);
-    int rv = d.alloc(W * (size_t)(P + 1));
-    if (rv != PR_OK) {
-      free_state(s);
-      return rv;
-    }
-    PR_HIP(hipMemcpyAsync(d.p, &rec, W, hipMemcpyHostToDevice, g->stream));
-    const ncclResult_t rc = ncclAllGather(d.p, (uint8_t *)d.p + W, W, ncclUint8, g->comm, g->stream);
-    if (rc != ncclSuccess) {
-      free_state(s);
-      return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
-    }
-    PR_HIP(hipMemcpyAsync(all.data(), (uint8_t *)d.p + W, W * (size_t)P, hipMemcpyDeviceToHost, g->stream));
+    uint8_t *d = static_cast<uint8_t *>(g->comm_scratch.p);
+    PR_HIP(hipMemcpyAsync(d, &rec, W, hipMemcpyHostToDevice, g->stream));
+    const ncclResult_t rc = ncclAllGather(d, d + W, W, ncclUint8, g->comm, g->stream);
+    if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
+    PR_HIP(hipMemcpyAsync(all.data(), d + W, W * (size_t)P, hipMemcpyDeviceToHost, g->stream));
     PR_HIP(hipStreamSynchronize(g->stream));
   }
   int32_t ok = 1;
@@ -305,17 +320,19 @@ int ipc_setup(pr_graph *g) {
   // every rank has opened every page: the names can go
   int32_t agreed = ok;
   const int rv = comm_barrier(g, &agreed);
-  if (s->mine) shm_unlink(s->page);
-  if (rv != PR_OK) {
-    free_state(s);
-    return rv;
+  if (s->mine) {
+    shm_unlink(s->page);
+    s->page[0] = 0;
   }
-  if (!agreed) {
-    free_state(s);
+  if (s == &dummy) {  // nothing of the stand-in may outlive this call (it holds no resources)
+    guard.s = nullptr;
+    return rv != PR_OK ? rv : fail(PR_ERR_OOM, "IPC exchange set-up failed on this rank: host allocation failed");
+  }
+  if (rv != PR_OK) return rv;
+  if (!agreed)
     return fail(PR_ERR_COMM, "IPC exchange set-up failed on " + std::string(ok ? "a peer" : "this rank") +
                                  (why.empty() ? std::string() : ": " + why));
-  }
-  g->ipc = s;
+  g->ipc = guard.release();
   return PR_OK;
 }
 
@@ -408,6 +425,20 @@ struct HipIpcOps {
     return PR_OK;
   }
 };
+
+bool stream_idle_within(hipStream_t st, double seconds) {
+  if (!st) return true;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e != hipErrorNotReady) {
+      (void)hipGetLastError();
+      return true;  // idle (or an error: nothing left to wait for)
+    }
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  }
+}
 
 // Before the compute stream writes the send runs of `buf` for the next exchange: order the writes
 // after every peer's copies of the previous exchange of `buf`.

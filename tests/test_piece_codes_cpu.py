@@ -24,10 +24,10 @@ PIECE_TBL = 256
 
 @pytest.fixture(scope="module")
 def shim():
-    if not os.path.exists(SHIM):
-        import subprocess
+    import subprocess
 
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host")], check=True)
+    # always: make's dependency on pr_pieces.h rebuilds a stale shim after an edit
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host")], check=True)
     lib = ctypes.CDLL(SHIM)
     P_ = ctypes.c_void_p
     lib.prp_tbl_words.restype = ctypes.c_int
