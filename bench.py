@@ -253,9 +253,11 @@ def contract_error_line(world: int, steps: int, warmup: int, msg: str) -> dict:
             "roofline": None, "cpu_baseline": None, "error": msg}
 
 
-EXCHANGE_MODES = [("unchunked", False, 0, False), ("chunked_reserve0", True, 0, False),
-                  ("chunked_reserve1", True, 1, False), ("chunked_reserve2", True, 2, False)]
-IPC_MODES = [("ipc_unchunked", False, 0, True), ("ipc_chunked", True, 0, True)]
+EXCHANGE_MODES = [("unchunked", False, 0, 0), ("chunked_reserve0", True, 0, 0),
+                  ("chunked_reserve1", True, 1, 0), ("chunked_reserve2", True, 2, 0)]
+# (name, chunked, CU reserve, IPC: 0 = RCCL, 1 = copy-engine pulls, 2 = pulls of each chunk as soon as
+# the peer's epilogue has written it -- per-chunk publication)
+IPC_MODES = [("ipc_unchunked", False, 0, 1), ("ipc_chunked", True, 0, 1), ("ipc_chunked_early", True, 0, 2)]
 
 
 def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chunks: int, device: str = "cuda",
@@ -546,7 +548,7 @@ def main() -> int:
     # candidate (max over ranks) is the configuration timed below; the parity leg then checks that
     # very configuration against the oracle (parity.timed_mode).
     overlap = None
-    mode = ("unchunked", False, 0, False)
+    mode = EXCHANGE_MODES[0]
     ipc_ok = False
     if dist is not None and info.get("classes", 1) >= 16 and not a.no_overlap_ab:
         wd.enter("calibration", limits["calibration"])
@@ -637,14 +639,12 @@ def main() -> int:
         # the RCCL unchunked exchange (the library default) is the reference every other mode must
         # equal bit for bit on every rank; then the timed configuration itself (its chunking, hot
         # reserve and transport), and every other transport setting the calibration could pick
-        ref_mode = ("unchunked", False, 0, False)
+        ref_mode = EXCHANGE_MODES[0]
         set_mode(ref_mode)
         ref_local, mine, owned_once = gpu_ranks()
         checked = {}  # name -> (merged ranks on rank 0, bitwise equal to the reference on every rank)
         if overlap is not None:
-            others = [mode] + [m for m in (("chunked_reserve0", True, 0, False), ("ipc_unchunked", False, 0, True),
-                                           ("ipc_chunked", True, 0, True))
-                               if m[0] != mode[0] and (ipc_ok or not m[3])]
+            others = [mode] + [m for m in [EXCHANGE_MODES[1]] + IPC_MODES if m[0] != mode[0] and (ipc_ok or not m[3])]
             for m in others:
                 if m[0] == ref_mode[0]:
                     continue
@@ -681,14 +681,13 @@ def main() -> int:
                     parity["modes"] = per_mode
                     if "chunked_reserve0" in per_mode:
                         parity["max_rel_overlapped_exchange"] = per_mode["chunked_reserve0"]["max_rel"]
-                    for nm in ("ipc_unchunked", "ipc_chunked"):
-                        if nm in per_mode:
-                            parity[f"{nm}_bitwise_equal_rccl"] = per_mode[nm]["bitwise_equal_rccl_unchunked"]
-                    if "ipc_unchunked" in per_mode and "ipc_chunked" in per_mode:
-                        parity["ipc_bitwise_equal_rccl"] = (parity["ipc_unchunked_bitwise_equal_rccl"]
-                                                            and parity["ipc_chunked_bitwise_equal_rccl"])
-                        parity["max_rel_ipc_exchange"] = max(per_mode["ipc_unchunked"]["max_rel"],
-                                                             per_mode["ipc_chunked"]["max_rel"])
+                    ipc_names = [m[0] for m in IPC_MODES if m[0] in per_mode]
+                    for nm in ipc_names:
+                        parity[f"{nm}_bitwise_equal_rccl"] = per_mode[nm]["bitwise_equal_rccl_unchunked"]
+                    if ipc_names:
+                        parity["ipc_bitwise_equal_rccl"] = all(per_mode[nm]["bitwise_equal_rccl_unchunked"]
+                                                               for nm in ipc_names)
+                        parity["max_rel_ipc_exchange"] = max(per_mode[nm]["max_rel"] for nm in ipc_names)
                 if world == 1 and K >= 2:
                     it_ms = res["iter_ms"][1:]
                     med = float(np.median(it_ms))

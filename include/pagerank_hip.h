@@ -181,7 +181,10 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
 #define PR_OPT_HOT_RESERVE 2
 /* PR_OPT_XCHG_IPC (RCCL path, ranks on one node): 1 = every rank pulls the runs it reads straight
  * out of its peers' send buffers (IPC-mapped) with the copy engines, ordered by interprocess
- * events, so no transfer kernel takes a CU from the SpMV; 0 = RCCL send/recv (the default).
+ * events, so no transfer kernel takes a CU from the SpMV; 0 = RCCL send/recv (the default);
+ * 2 = as 1, and the epilogue runs chunk by chunk, publishing each chunk's runs as soon as they are
+ * written, so (with PR_OPT_XCHG_CHUNKS) a peer's pull of chunk c overlaps this rank's epilogue of
+ * the later chunks (the split layout's fused pack with several chunks; otherwise as 1).
  * Collective like PR_OPT_XCHG_CHUNKS (which it combines with); the first enable maps the peers'
  * buffers and fails with PR_ERR_COMM on every rank if any rank cannot. */
 #define PR_OPT_XCHG_IPC 3

@@ -295,8 +295,9 @@ int pr_set_option(pr_graph *g, int32_t option, int64_t value) {
     return PR_OK;
   }
   if (option == PR_OPT_XCHG_IPC) {
-    if (value != 0 && value != 1) return fail(PR_ERR_INVALID, "PR_OPT_XCHG_IPC: 0 (RCCL) or 1 (IPC copy engines)");
-    return pr::set_exchange_ipc(g, value == 1);
+    if (value < 0 || value > 2)
+      return fail(PR_ERR_INVALID, "PR_OPT_XCHG_IPC: 0 (RCCL), 1 (IPC copy engines) or 2 (IPC, per-chunk publication)");
+    return pr::set_exchange_ipc(g, (int)value);
   }
   if (option != PR_OPT_XCHG_CHUNKS) return fail(PR_ERR_INVALID, "unknown option");
   PR_TRY(pr::join_exchange(g));  // a pending overlapped exchange finishes under the old setting
@@ -532,6 +533,7 @@ void pr_graph_destroy(pr_graph *g) {
   if (g->xev) (void)hipEventDestroy(g->xev);
   for (hipEvent_t e : g->x_ev) (void)hipEventDestroy(e);
   if (g->x_pack_ev) (void)hipEventDestroy(g->x_pack_ev);
+  if (g->x_free_ev) (void)hipEventDestroy(g->x_free_ev);
   if (g->xstream) (void)hipStreamDestroy(g->xstream);
   g->ev_pool.clear();
   hipStream_t s = g->stream;

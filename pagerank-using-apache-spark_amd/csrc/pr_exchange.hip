@@ -309,6 +309,7 @@ int build_exchange(pr_graph *g, const uint64_t *ukeys, int64_t m, int b, uint64_
   g->x_ev.assign(g->n_xc, nullptr);
   for (auto &e : g->x_ev) PR_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   PR_HIP(hipEventCreateWithFlags(&g->x_pack_ev, hipEventDisableTiming));
+  PR_HIP(hipEventCreateWithFlags(&g->x_free_ev, hipEventDisableTiming));
   // fused pack: the split epilogue writes the runs itself (P <= 8: the row mask is one byte)
   g->x_fused = false;
   if (g->opts.pack_fused && g->C > 1 && P <= kMaxPackParts && g->x_soff[P] > 0) PR_TRY(build_fused_pack(g));

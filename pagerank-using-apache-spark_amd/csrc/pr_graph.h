@@ -168,6 +168,13 @@ struct pr_graph {
   // of its peers' IPC-mapped send buffers with the copy engines
   pr::IpcState *ipc = nullptr;  // mapped on first use, kept until destroy
   bool x_ipc = false;           // exchanges use it
+  // PR_OPT_XCHG_IPC = 2: the epilogue runs chunk by chunk and publishes each chunk's send runs as
+  // soon as they are written (per-chunk sent records, pr_ipc_protocol.h), so the peers' pulls of
+  // chunk c overlap this rank's epilogue of the later chunks
+  bool x_ipc_early = false;
+  // recorded on the compute stream when the gather buffer the next exchange fills is no longer read
+  // (the start of an iteration / reset): the IPC copy streams wait for it, not for the whole pass
+  hipEvent_t x_free_ev = nullptr;
 
   // RCCL (one process per GPU)
   ncclComm_t comm = nullptr;
@@ -184,7 +191,7 @@ struct pr_graph {
 };
 
 namespace pr {
-constexpr size_t kCommScratchBytes = 128 << 10;
+constexpr size_t kCommScratchBytes = 256 << 10;
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (after rmask/cbase)
@@ -215,8 +222,10 @@ int verify_exchange(pr_graph *g);  // after ncclCommInitRank
 int read_slots(pr_graph *g, int buf, double *dc, double *l1);
 // IPC transport (pr_ipc.hip): collective switch; the reuse wait before the send runs of buf are
 // written (no-op unless x_ipc); the exchange itself; unmapping at destroy
-int set_exchange_ipc(pr_graph *g, bool on);
+int set_exchange_ipc(pr_graph *g, int mode);  // 0: RCCL, 1: IPC, 2: IPC with per-chunk publication
 int ipc_send_runs_free(pr_graph *g, int buf);
+bool ipc_early(const pr_graph *g);               // the epilogue publishes chunk by chunk
+int ipc_chunk_sent(pr_graph *g, int buf, int c);  // the epilogue wrote the runs of chunk c of buf
 int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b);
 void ipc_destroy(pr_graph *g);
 bool stream_idle_within(hipStream_t s, double seconds);  // host poll of hipStreamQuery with a deadline

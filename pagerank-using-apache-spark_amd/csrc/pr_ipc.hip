@@ -10,12 +10,15 @@
 //            with hipMemcpyDeviceToDeviceNoCU on a copy stream of its own per peer (the peers' runs
 //            move at once, over their own links), chunk by chunk; the transfer stream (xstream)
 //            joins every peer's chunk c before it records x_ev[c], as the RCCL exchange does.
-//   device   two interprocess events per buffer b and rank: `sent[b]` (recorded on the owner's
-//            compute stream once the runs of b are written: fused epilogue + k_finalize, or k_pack)
-//            and `copied[b]` (recorded on the owner's xstream after its copies out of every peer's
-//            runs of b).  A receiver's xstream waits for every peer's sent[b] before copying; an
-//            owner's compute stream waits for every peer's copied[b] of the previous exchange of b
-//            before it writes the runs of b again (the reuse hazard of the double buffer).
+//   device   interprocess events per buffer b and rank: `sent[b][c]` per exchange chunk c
+//            (recorded on the owner's compute stream once chunk c of the runs of b is written: with
+//            PR_OPT_XCHG_IPC = 2 right after the epilogue chunk that wrote it, otherwise all at the
+//            end of the pass -- fused epilogue + k_finalize, or k_pack) and `copied[b]` (recorded
+//            on the owner's xstream after its copies out of every peer's runs of b).  A receiver's
+//            copy stream waits for a peer's sent[b][c] before copying chunk c (whole runs: the last
+//            chunk's record, which implies the others); an owner's compute stream waits for every
+//            peer's copied[b] of the previous exchange of b before it writes the runs of b again
+//            (the reuse hazard of the double buffer).
 //   host     a wait on an interprocess event binds to the latest record *enqueued so far*, so the
 //            waiter's host must not enqueue it before the owner's host has enqueued the record it
 //            means.  Every rank publishes, in a small shared-memory page of its own, how many
@@ -54,6 +57,7 @@ int64_t send_stride(const pr_graph *g);   // pr_exchange.hip
 namespace {
 
 constexpr double kSpinLimit = 120.0;  // seconds a host waits for a peer's record before failing
+constexpr int kIpcMaxChunks = 16;     // sent events per buffer: one per exchange chunk (C / 8 <= 16)
 
 // one rank's shared-memory page: how many sent[b] / copied[b] records it has enqueued
 struct alignas(64) IpcCounters {
@@ -65,7 +69,7 @@ static_assert(std::atomic<int64_t>::is_always_lock_free, "cross-process counters
 // what every rank publishes at set-up (ncclAllGather of bytes)
 struct IpcRecord {
   hipIpcMemHandle_t mem;         // its x_sbuf
-  hipIpcEventHandle_t sent[2];   // its sent[b]
+  hipIpcEventHandle_t sent[2][kIpcMaxChunks];  // its sent[b] per chunk
   hipIpcEventHandle_t copied[2];  // its copied[b]
   char page[64];                 // its counter page (shm_open name)
   int64_t stride;                // doubles per send buffer (send_stride)
@@ -86,8 +90,10 @@ struct IpcState {
   std::vector<void *> peer_sbuf;      // mapped send buffers
   std::vector<int64_t> peer_stride;   // doubles per peer send buffer
   std::vector<int64_t> peer_soff_me;  // start of the peer's run for this rank
-  hipEvent_t sent[2] = {nullptr, nullptr}, copied[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> peer_sent, peer_copied;  // [q * 2 + b]
+  std::vector<hipEvent_t> sent;  // [b * nc + c]
+  hipEvent_t copied[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> peer_sent;    // [(q * 2 + b) * nc + c]
+  std::vector<hipEvent_t> peer_copied;  // [q * 2 + b]
   // one copy stream per peer, so the runs of different peers move at once (on their own copy
   // engines / xGMI links), and per (peer, chunk) the event the transfer stream joins on
   std::vector<hipStream_t> cstream;
@@ -136,10 +142,10 @@ void free_state(IpcState *s) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : s->peer_copied)
     if (e) (void)hipEventDestroy(e);
-  for (int b = 0; b < 2; ++b) {
-    if (s->sent[b]) (void)hipEventDestroy(s->sent[b]);
+  for (hipEvent_t e : s->sent)
+    if (e) (void)hipEventDestroy(e);
+  for (int b = 0; b < 2; ++b)
     if (s->copied[b]) (void)hipEventDestroy(s->copied[b]);
-  }
   for (IpcCounters *c : s->peer) unmap_page(c);
   if (s->mine) {
     unmap_page(s->mine);
@@ -231,11 +237,14 @@ int ipc_setup(pr_graph *g) {
   s->peer_sbuf.assign(P, nullptr);
   s->peer_stride.assign(P, 0);
   s->peer_soff_me.assign(P, 0);
-  s->peer_sent.assign(2 * (size_t)P, nullptr);
+  s->nc = g->n_xc;
+  s->proto.nc = s->nc;
+  s->sent.assign(2 * (size_t)s->nc, nullptr);
+  s->peer_sent.assign(2 * (size_t)P * s->nc, nullptr);
   s->peer_copied.assign(2 * (size_t)P, nullptr);
   s->cstream.assign(P, nullptr);
-  s->nc = g->n_xc;
   s->cev.assign((size_t)P * s->nc, nullptr);
+  local(s->nc >= 1 && s->nc <= kIpcMaxChunks, "exchange chunk count out of range");
   if (rec.ok) {
     std::snprintf(s->page, sizeof(s->page), "/pr_xipc_%d_%d_%llx", (int)getpid(), self,
                   (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
@@ -245,13 +254,15 @@ int ipc_setup(pr_graph *g) {
   }
   if (rec.ok) local(hipIpcGetMemHandle(&rec.mem, g->x_sbuf.p) == hipSuccess, "hipIpcGetMemHandle failed");
   for (int b = 0; b < 2 && rec.ok; ++b) {
-    local(hipEventCreateWithFlags(&s->sent[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&s->copied[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
+    local(hipEventCreateWithFlags(&s->copied[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
           "hipEventCreateWithFlags(hipEventInterprocess) failed");
-    if (rec.ok)
-      local(hipIpcGetEventHandle(&rec.sent[b], s->sent[b]) == hipSuccess &&
-                hipIpcGetEventHandle(&rec.copied[b], s->copied[b]) == hipSuccess,
-            "hipIpcGetEventHandle failed");
+    if (rec.ok) local(hipIpcGetEventHandle(&rec.copied[b], s->copied[b]) == hipSuccess, "hipIpcGetEventHandle failed");
+    for (int c = 0; c < s->nc && rec.ok; ++c) {
+      hipEvent_t &e = s->sent[(size_t)b * s->nc + c];
+      local(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
+            "hipEventCreateWithFlags(hipEventInterprocess) failed");
+      if (rec.ok) local(hipIpcGetEventHandle(&rec.sent[b][c], e) == hipSuccess, "hipIpcGetEventHandle failed");
+    }
   }
   rec.stride = send_stride(g);
   for (int q = 0; q <= P; ++q) rec.soff[q] = g->x_soff[q];
@@ -290,12 +301,17 @@ int ipc_setup(pr_graph *g) {
       break;
     }
     for (int b = 0; b < 2 && ok; ++b) {
-      if (hipIpcOpenEventHandle(&s->peer_sent[2 * q + b], r.sent[b]) != hipSuccess ||
-          hipIpcOpenEventHandle(&s->peer_copied[2 * q + b], r.copied[b]) != hipSuccess) {
+      if (hipIpcOpenEventHandle(&s->peer_copied[2 * q + b], r.copied[b]) != hipSuccess) {
         (void)hipGetLastError();
         ok = 0;
         why = "hipIpcOpenEventHandle failed";
       }
+      for (int c = 0; c < s->nc && ok; ++c)
+        if (hipIpcOpenEventHandle(&s->peer_sent[((size_t)q * 2 + b) * s->nc + c], r.sent[b][c]) != hipSuccess) {
+          (void)hipGetLastError();
+          ok = 0;
+          why = "hipIpcOpenEventHandle failed";
+        }
     }
     if (ok && hipStreamCreateWithFlags(&s->cstream[q], hipStreamNonBlocking) != hipSuccess) {
       (void)hipGetLastError();
@@ -338,8 +354,12 @@ int ipc_setup(pr_graph *g) {
 
 }  // namespace
 
-int set_exchange_ipc(pr_graph *g, bool on) {
-  if (on == g->x_ipc) return PR_OK;
+int set_exchange_ipc(pr_graph *g, int mode) {
+  const bool on = mode != 0;
+  if (on == g->x_ipc) {
+    g->x_ipc_early = mode == 2;  // per-chunk publication: no effect on the ordering state
+    return PR_OK;
+  }
   if (on) {
     if (!g->comm || g->comm_size <= 1) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs an attached communicator (P > 1)");
     if (g->x_allgather) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs the per-peer runs (PR_BOPT_EXCHANGE = 0)");
@@ -358,8 +378,11 @@ int set_exchange_ipc(pr_graph *g, bool on) {
   }
   PR_TRY(comm_barrier(g, &one));
   g->x_ipc = on;
+  g->x_ipc_early = mode == 2;
   return PR_OK;
 }
+
+bool ipc_early(const pr_graph *g) { return g->x_ipc && g->x_ipc_early && g->ipc && g->x_fused && g->n_xc > 1; }
 
 // The HIP side of the protocol's steps: interprocess events, the counter pages, the copy streams.
 struct HipIpcOps {
@@ -367,61 +390,64 @@ struct HipIpcOps {
   IpcState *s;
   hipEvent_t ev_a;  // timing: recorded on the transfer stream before the copies (may be null)
 
-  hipEvent_t peer_event(int q, int kind, int b) const {
-    return kind == kIpcSent ? s->peer_sent[2 * q + b] : s->peer_copied[2 * q + b];
-  }
   int spin(int q, int kind, int b, int64_t v) {
     const std::atomic<int64_t> &c = kind == kIpcSent ? s->peer[q]->sent[b] : s->peer[q]->copied[b];
     return spin_until(c, v, kind == kIpcSent ? "sent" : "copied", q);
   }
-  int wait_compute(int q, int kind, int b, int64_t) {
-    PR_HIP(hipStreamWaitEvent(g->stream, peer_event(q, kind, b), 0));
+  int wait_compute(int q, int kind, int b, int, int64_t) {
+    if (kind != kIpcCopied) return fail("IPC exchange: the compute stream only waits for copied records");
+    PR_HIP(hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + b], 0));
     return PR_OK;
   }
-  int wait_copy(int q, int kind, int b, int64_t) {
-    PR_HIP(hipStreamWaitEvent(s->cstream[q], peer_event(q, kind, b), 0));
+  int wait_copy(int q, int kind, int b, int c, int64_t) {
+    if (kind != kIpcSent) return fail("IPC exchange: a copy stream only waits for sent records");
+    PR_HIP(hipStreamWaitEvent(s->cstream[q], s->peer_sent[((size_t)q * 2 + b) * s->nc + c], 0));
     return PR_OK;
   }
-  int record(int kind, int b, int64_t k) {
-    if (kind == kIpcSent) {  // the runs of b are written: after the pass (+ pack) on the compute stream
-      PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));
-      PR_HIP(hipEventRecord(s->sent[b], g->stream));
-      s->mine->sent[b].store(k, std::memory_order_release);
+  int record(int kind, int b, int c, int64_t) {
+    if (kind == kIpcSent) {  // chunk c of the runs of b is written (compute stream)
+      if (c == s->nc - 1) PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));  // the whole pass (+ pack) is done
+      PR_HIP(hipEventRecord(s->sent[(size_t)b * s->nc + c], g->stream));
     } else {  // the transfer stream has joined every copy of b
       PR_HIP(hipEventRecord(s->copied[b], g->xstream));
-      s->mine->copied[b].store(k, std::memory_order_release);
     }
+    return PR_OK;
+  }
+  int publish(int kind, int b, int64_t k) {
+    (kind == kIpcSent ? s->mine->sent[b] : s->mine->copied[b]).store(k, std::memory_order_release);
     return PR_OK;
   }
   int pack(int b) { return exchange_pack(g, b); }
   int fail(const char *msg) { return pr::fail(PR_ERR_STATE, msg); }
 
-  // every copy stream waits until this rank's pass no longer reads cbuf[b]; then per chunk the
-  // copies of every peer, each joined by the transfer stream before it records x_ev[c]
-  int copies(int b) {
+  int copy_steps() const { return g->x_chunked ? s->nc : 1; }
+  // the transfer stream joins this rank's pass (timing: pack done -> last chunk in); every copy
+  // stream waits only until this rank no longer reads gather buffer b (x_free_ev, recorded before
+  // the pass), so a peer's chunk can land while this rank's own epilogue still runs
+  int copy_begin(int) {
+    if (g->n_xc != s->nc) return fail("IPC exchange: chunk count changed");
     PR_HIP(hipStreamWaitEvent(g->xstream, g->x_pack_ev, 0));
     if (ev_a) PR_HIP(hipEventRecord(ev_a, g->xstream));
     for (int q = 0; q < s->P; ++q)
-      if (q != s->self) PR_HIP(hipStreamWaitEvent(s->cstream[q], g->x_pack_ev, 0));
-    const int nc = g->n_xc, steps = g->x_chunked ? nc : 1;
-    if (nc != s->nc) return fail("IPC exchange: chunk count changed");
-    double *base = g->cbuf[b].as<double>();
-    for (int c = 0; c < steps; ++c) {
-      const int lo = g->x_chunked ? c : 0, hi = g->x_chunked ? c + 1 : nc;
-      for (int q = 0; q < s->P; ++q) {
-        if (q == s->self) continue;
-        const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
-        if (r1 <= r0) continue;
-        const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(b & 1) * s->peer_stride[q] +
-                            s->peer_soff_me[q] + r0;
-        PR_HIP(hipMemcpyAsync(base + g->S_pad + g->x_roff[q] + r0, src, sizeof(double) * (size_t)(r1 - r0),
-                              hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
-        hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
-        PR_HIP(hipEventRecord(e, s->cstream[q]));
-        PR_HIP(hipStreamWaitEvent(g->xstream, e, 0));  // chunk c of every peer -> x_ev[c]
-      }
-      PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
+      if (q != s->self) PR_HIP(hipStreamWaitEvent(s->cstream[q], g->x_free_ev, 0));
+    return PR_OK;
+  }
+  int copy(int q, int b, int lo, int hi) {
+    const int nc = s->nc;
+    const int64_t r0 = g->x_rch[(size_t)q * (nc + 1) + lo], r1 = g->x_rch[(size_t)q * (nc + 1) + hi];
+    if (r1 > r0) {
+      const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(b & 1) * s->peer_stride[q] +
+                          s->peer_soff_me[q] + r0;
+      PR_HIP(hipMemcpyAsync(g->cbuf[b].as<double>() + g->S_pad + g->x_roff[q] + r0, src,
+                            sizeof(double) * (size_t)(r1 - r0), hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
     }
+    hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
+    PR_HIP(hipEventRecord(e, s->cstream[q]));
+    PR_HIP(hipStreamWaitEvent(g->xstream, e, 0));  // chunk hi - 1 of every peer -> x_ev[hi - 1]
+    return PR_OK;
+  }
+  int step_done(int, int hi) {
+    PR_HIP(hipEventRecord(g->x_ev[hi - 1], g->xstream));
     return PR_OK;
   }
 };
@@ -446,6 +472,11 @@ int ipc_send_runs_free(pr_graph *g, int buf) {
   if (!g->x_ipc) return PR_OK;
   HipIpcOps o{g, g->ipc, nullptr};
   return g->ipc->proto.send_runs_free(o, buf);
+}
+
+int ipc_chunk_sent(pr_graph *g, int buf, int c) {
+  HipIpcOps o{g, g->ipc, nullptr};
+  return g->ipc->proto.chunk_sent(o, buf, c);
 }
 
 int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {

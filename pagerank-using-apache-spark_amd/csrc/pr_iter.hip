@@ -283,6 +283,7 @@ int iter_reset(pr_graph *g, const double *init_host) {
   }
   g->cur = 0;
   g->x_packed = -1;
+  if (g->x_free_ev) PR_HIP(hipEventRecord(g->x_free_ev, s));  // the exchange below fills buffer 0
   PR_TRY(ipc_send_runs_free(g, 0));  // k_finalize below writes the slots of the runs of buffer 0
   const int64_t own = g->own_off;
   hipLaunchKernelGGL(k_reset, dim3(g->reset_blocks), dim3(kThreads), 0, s, g->n_rows,
@@ -334,6 +335,8 @@ int iter_compute(pr_graph *g) {
     open_ev = (int)g->ev_next - 1;  // a following interval may start where this one ended
     return PR_OK;
   };
+  // the gather buffer this iteration's exchange fills (`out`) was last read by the previous pass
+  if (g->x_free_ev) PR_HIP(hipEventRecord(g->x_free_ev, s));
   PR_TRY(ipc_send_runs_free(g, out));  // the epilogue and k_finalize write the runs of `out`
   const int nph = g->C > 1 ? n_hot_phases(g) : 1;
   const bool phased_wait = g->C > 1 && g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1;
@@ -375,12 +378,35 @@ int iter_compute(pr_graph *g) {
       pd.self = g->part;
       for (int q = 0; q < g->nparts; ++q) pd.soff[q] = g->x_soff[q];
     }
-    hipLaunchKernelGGL(epi, dim3(g->ep_blocks), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
-                       g->nblk, (int64_t)0, (g->nblk + kEpiGroup - 1) / kEpiGroup, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(), g->rowinfo.as<uint32_t>(),
-                       g->r.as<double>(), g->cbuf[out].as<double>() + own, g->cbuf[in].as<double>(), g->slots,
-                       (double)g->V, g->teleport, g->damping, g->unit_part.as<double2>() + g->n_units,
-                       g->eoff.as<int64_t>(), g->epos.as<uint16_t>(), g->x_pmask.as<uint8_t>(),
-                       g->x_sbase.as<int32_t>(), pd);
+    auto epilogue = [&](int64_t g_lo, int64_t g_hi, unsigned grid) -> int {
+      hipLaunchKernelGGL(epi, dim3(grid), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
+                         g->nblk, g_lo, g_hi, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(),
+                         g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
+                         g->cbuf[in].as<double>(), g->slots, (double)g->V, g->teleport, g->damping,
+                         g->unit_part.as<double2>() + g->n_units, g->eoff.as<int64_t>(), g->epos.as<uint16_t>(),
+                         g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(), pd);
+      PR_HIP(hipGetLastError());
+      return PR_OK;
+    };
+    const int64_t ngrp = epi_groups(g);
+    if (!ipc_early(g)) {
+      PR_TRY(epilogue(0, ngrp, (unsigned)g->ep_blocks));
+    } else {
+      // PR_OPT_XCHG_IPC = 2: chunk c of the send runs holds the rows of class regions [8c, 8c + 8),
+      // local rows [8c Q_pad, (8c + 8) Q_pad): the epilogue runs over the groups that end them, and
+      // the chunk is published as soon as it is written (its peers' pulls then overlap the rest of
+      // the epilogue); the last chunk carries the slots k_finalize writes and goes with the exchange
+      const int64_t rows_per_grp = (int64_t)kEpiGroup * kWave, chunk_rows = (int64_t)kXcds * g->Q_pad;
+      const int wpb = epi_grp_threads(g->epi_narrow) / kWave;
+      int64_t g_lo = 0;
+      for (int c = 0; c < g->n_xc; ++c) {
+        const int64_t g_hi = c == g->n_xc - 1 ? ngrp
+                                               : std::min(ngrp, ((int64_t)(c + 1) * chunk_rows + rows_per_grp - 1) / rows_per_grp);
+        if (g_hi > g_lo) PR_TRY(epilogue(g_lo, g_hi, grid_for(g_hi - g_lo, wpb, 1u << 20)));
+        g_lo = std::max(g_lo, g_hi);
+        if (c < g->n_xc - 1) PR_TRY(ipc_chunk_sent(g, out, c));
+      }
+    }
     n_parts += epi_groups(g);
   }
   PR_HIP(hipGetLastError());

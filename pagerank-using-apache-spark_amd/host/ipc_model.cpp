@@ -21,19 +21,23 @@
 
 namespace {
 
+constexpr int kMaxChunks = 16;
+
 struct World {
-  int P;
-  // per (rank, kind, buffer): records enqueued ("latest record") and the published counter
+  int P, nc;
+  // per (rank, kind, buffer, chunk): records enqueued ("latest record"); per (rank, kind, buffer):
+  // the published counter
   std::vector<std::atomic<int64_t>> enq, pub;
   std::mutex mu;
   std::string err;
   std::atomic<bool> failed{false};
   std::atomic<int64_t> waits{0};
-  explicit World(int p) : P(p), enq(4 * (size_t)p), pub(4 * (size_t)p) {
+  World(int p, int c) : P(p), nc(c), enq(4 * (size_t)p * kMaxChunks), pub(4 * (size_t)p) {
     for (auto &a : enq) a.store(0);
     for (auto &a : pub) a.store(0);
   }
   size_t ix(int r, int kind, int b) const { return (size_t)r * 4 + (size_t)kind * 2 + (size_t)b; }
+  size_t ex(int r, int kind, int b, int c) const { return ix(r, kind, b) * kMaxChunks + (size_t)c; }
   int fail(const std::string &m) {
     std::lock_guard<std::mutex> g(mu);
     if (err.empty()) err = m;
@@ -47,7 +51,8 @@ struct ModelOps {
   int self;
   std::mt19937_64 rng;
   int max_delay_us;
-  bool broken;  // checker self-test: no host spin before the sent waits
+  bool broken;     // checker self-test: no host spin before the sent waits
+  int steps = 1;   // copy steps of the current exchange (1: whole runs; nc: per chunk)
 
   void delay() {
     if (max_delay_us <= 0) return;
@@ -71,22 +76,33 @@ struct ModelOps {
     delay();
     return 0;
   }
-  int wait_any(int q, int kind, int b, int64_t v) {
-    const int64_t latest = w->enq[w->ix(q, kind, b)].load(std::memory_order_acquire);
+  int wait_any(int q, int kind, int b, int c, int64_t v) {
+    const int64_t latest = w->enq[w->ex(q, kind, b, c)].load(std::memory_order_acquire);
     w->waits.fetch_add(1);
     if (latest != v)
       return w->fail("rank " + std::to_string(self) + " waits on rank " + std::to_string(q) + "'s " +
-                     (kind == pr::kIpcSent ? "sent" : "copied") + "[" + std::to_string(b) + "] meaning record " +
-                     std::to_string(v) + " but its latest record is " + std::to_string(latest));
+                     (kind == pr::kIpcSent ? "sent" : "copied") + "[" + std::to_string(b) + "] chunk " +
+                     std::to_string(c) + " meaning record " + std::to_string(v) + " but its latest record is " +
+                     std::to_string(latest));
     delay();
     return 0;
   }
-  int wait_compute(int q, int kind, int b, int64_t v) { return wait_any(q, kind, b, v); }
-  int wait_copy(int q, int kind, int b, int64_t v) { return wait_any(q, kind, b, v); }
-  int record(int kind, int b, int64_t k) {
-    const int64_t e = w->enq[w->ix(self, kind, b)].fetch_add(1) + 1;
-    if (e != k) return w->fail("rank " + std::to_string(self) + " enqueued record " + std::to_string(e) + " as " + std::to_string(k));
+  int wait_compute(int q, int kind, int b, int c, int64_t v) { return wait_any(q, kind, b, c, v); }
+  int wait_copy(int q, int kind, int b, int c, int64_t v) { return wait_any(q, kind, b, c, v); }
+  int record(int kind, int b, int c, int64_t k) {
+    const int64_t e = w->enq[w->ex(self, kind, b, c)].fetch_add(1) + 1;
+    if (e != k)
+      return w->fail("rank " + std::to_string(self) + " enqueued record " + std::to_string(e) + " of chunk " +
+                     std::to_string(c) + " as " + std::to_string(k));
     delay();
+    return 0;
+  }
+  int publish(int kind, int b, int64_t k) {
+    const int n = kind == pr::kIpcSent ? w->nc : 1;
+    for (int c = 0; c < n; ++c)  // every chunk's record k is enqueued before k is published
+      if (w->enq[w->ex(self, kind, b, c)].load() != k)
+        return w->fail("rank " + std::to_string(self) + " published " + std::to_string(k) + " before chunk " +
+                       std::to_string(c) + "'s record");
     w->pub[w->ix(self, kind, b)].store(k, std::memory_order_release);
     delay();
     return 0;
@@ -95,10 +111,13 @@ struct ModelOps {
     delay();
     return 0;
   }
-  int copies(int) {
+  int copy_steps() const { return steps; }
+  int copy_begin(int) { return 0; }
+  int copy(int, int, int, int) {
     delay();
     return 0;
   }
+  int step_done(int, int) { return 0; }
   int fail(const char *m) { return w->fail(m); }
 };
 
@@ -106,16 +125,21 @@ struct ModelOps {
 
 extern "C" {
 
-// P ranks run n_ops steps each (seeded: 0 = reset, which writes and exchanges buffer 0 with the
-// pack kernel; otherwise an iteration, whose pass writes the runs of the other buffer, packed or
-// not); returns the number of stream waits checked, or -1 with the first violation in err.
+// P ranks, nc sent chunks per buffer, run n_ops steps each (seeded, the same sequence on every
+// rank: 0 = reset, which writes and exchanges buffer 0 with the pack kernel; otherwise an
+// iteration whose pass writes the runs of the other buffer -- unfused (pack kernel), fused, or
+// fused with its chunks recorded one by one during the pass -- and whose copies go whole or per
+// chunk); returns the number of stream waits checked, or -1 with the first violation in err.
 // max_delay_us < 0: the checker's self-test -- the same run with the sent spins left out.
-int64_t ipc_model_run(int P, int n_ops, uint64_t seed, int max_delay_us, char *err, int errlen) {
-  if (P < 2 || P > 64 || n_ops < 0) return -1;
+int64_t ipc_model_run(int P, int nc, int n_ops, uint64_t seed, int max_delay_us, char *err, int errlen) {
+  if (P < 2 || P > 64 || nc < 1 || nc > kMaxChunks || n_ops < 0) return -1;
   std::mt19937_64 ops_rng(seed);
-  std::vector<int> ops((size_t)n_ops);
-  for (auto &o : ops) o = (int)(ops_rng() % 8);  // 0: reset, 1..7: iterations (1: unfused pack)
-  World w(P);
+  std::vector<int> ops((size_t)n_ops), steps((size_t)n_ops);
+  for (size_t i = 0; i < ops.size(); ++i) {
+    ops[i] = (int)(ops_rng() % 8);  // 0: reset, 1: unfused pack, 2..4: fused, 5..7: fused + early chunks
+    steps[i] = (ops_rng() & 1) ? nc : 1;
+  }
+  World w(P, nc);
   std::vector<std::thread> th;
   for (int r = 0; r < P; ++r)
     th.emplace_back([&, r]() {
@@ -124,8 +148,11 @@ int64_t ipc_model_run(int P, int n_ops, uint64_t seed, int max_delay_us, char *e
       pr::IpcProtocol<ModelOps> proto;
       proto.P = P;
       proto.self = r;
+      proto.nc = nc;
       int cur = 0;
-      for (int op : ops) {
+      for (size_t i = 0; i < ops.size(); ++i) {
+        const int op = ops[i];
+        o.steps = steps[i];
         if (w.failed.load()) return;
         int rv;
         if (op == 0) {  // pr_reset: k_finalize writes the slots of buffer 0's runs, then exchange(0)
@@ -135,6 +162,10 @@ int64_t ipc_model_run(int P, int n_ops, uint64_t seed, int max_delay_us, char *e
         } else {  // an iteration: the pass writes the runs of `out` (fused) unless op == 1
           const int out = cur ^ 1;
           rv = proto.send_runs_free(o, out);
+          for (int c = 0; rv == 0 && op >= 5 && c < nc - 1; ++c) {  // epilogue chunk c done
+            o.delay();
+            rv = proto.chunk_sent(o, out, c);
+          }
           if (rv == 0) rv = proto.exchange(o, out, op != 1);
           cur = out;
         }

@@ -214,12 +214,16 @@ class PageRankGraph:
         """pr_set_option(PR_OPT_HOT_RESERVE): CUs per XCD the heavy SpMV kernel leaves free."""
         check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_HOT_RESERVE, int(cus_per_xcd)))
 
-    def set_exchange_ipc(self, on: bool) -> None:
+    def set_exchange_ipc(self, mode) -> None:
         """pr_set_option(PR_OPT_XCHG_IPC): RCCL path on one node -- every rank pulls the runs it reads
-        out of its peers' IPC-mapped send buffers with the copy engines (True) or RCCL send/recv
-        (False, the default).  Collective: every rank calls it; the first enable maps the peers'
-        buffers and raises on every rank if any rank cannot."""
-        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_IPC, 1 if on else 0))
+        out of its peers' IPC-mapped send buffers with the copy engines (True / 1) or RCCL send/recv
+        (False / 0, the default); 2: IPC with the epilogue publishing chunk by chunk, so the peers'
+        pulls of a chunk overlap the rest of the epilogue.  Collective: every rank calls it; the first
+        enable maps the peers' buffers and raises on every rank if any rank cannot."""
+        v = int(mode)
+        if v not in (0, 1, 2):
+            raise ValueError("exchange ipc mode must be 0, 1 or 2")
+        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_IPC, v))
 
     # -- multi-process -------------------------------------------------------------------------
     def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:

@@ -34,7 +34,7 @@ class FakeGraph:
 
     def mode(self):
         if self.ipc:
-            return "ipc_chunked" if self.chunked else "ipc_unchunked"
+            return ("ipc_chunked_early" if self.ipc == 2 else "ipc_chunked") if self.chunked else "ipc_unchunked"
         return f"chunked_reserve{self.reserve}" if self.chunked else "unchunked"
 
     def set_exchange_ipc(self, on):
@@ -120,7 +120,7 @@ def test_all_modes_agree_and_are_candidates():
     ov = r0["overlap"]
     assert r0["ipc_ok"] and "rejected" not in ov and "ipc_error" not in ov
     for name in ("unchunked", "chunked_reserve0", "chunked_reserve1", "chunked_reserve2", "ipc_unchunked",
-                 "ipc_chunked"):
+                 "ipc_chunked", "ipc_chunked_early"):
         assert ov[f"{name}_ms_per_step"] > 0
     assert ov["candidates_bitwise_checked"] is True
 

@@ -58,6 +58,33 @@ __global__ __launch_bounds__(256) void k_ta_probe(const double *__restrict__ tab
   }
   if (acc == 12345.0) out[t] = acc;
 }
+// Line-sharing probe: random 8-byte loads where several accesses hit the same 128-byte line.
+//   MODE 0: g consecutive lanes of one instruction read g different words of one line
+//   MODE 1: each lane's g consecutive instructions read g different words of one line (the
+//           line is an L2 hit the first time, then a vector-L1 hit while it stays there)
+// Cost per instruction vs g says whether k_spmv_hot's cold gathers would get cheaper if the sources
+// a segment reads sat side by side in the gather space (the TA/TCP cost is per distinct line?).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_line_probe(const double *__restrict__ table, uint32_t n_lines, int64_t n_threads,
+                                                    uint32_t seed, int g, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_threads) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, n_lines * 128u, 0x00020000);
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint32_t w;
+    if constexpr (MODE == 0) {
+      const uint32_t grp = (uint32_t)(t - lane) + (uint32_t)(lane / g);
+      w = (mix32(grp * 8u + j + seed) % n_lines) * 16u + (uint32_t)(lane % g);
+    } else {
+      w = (mix32((uint32_t)t * 8u + (uint32_t)(j / g) + seed) % n_lines) * 16u + (uint32_t)(j % g);
+    }
+    acc += __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, w * 8u, 0, 0));
+  }
+  if (acc == 12345.0) out[t] = acc;
+}
 // Stream probe: every thread issues 8 coalesced buffer loads (or stores) of W bytes per lane; a
 // wave's lanes cover one contiguous 64 W-byte run per instruction, the table wrapping (2 MiB: L2
 // resident; 1 GiB: HBM).  Lanes >= active are exec-masked.  Time per instruction vs W and active
@@ -223,6 +250,40 @@ int prd_ta_probe(int device, int64_t table_bytes, int64_t n_loads, int active, i
     for (int i = 0; i < (rep ? iters : 1); ++i) {
       if (masked) hipLaunchKernelGGL(k_ta_probe<true>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
       else hipLaunchKernelGGL(k_ta_probe<false>, grid, dim3(256), 0, 0, (const double *)tab, nw, nt, 977u * i, active, (double *)out);
+    }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
+  return 0;
+}
+
+// Line-sharing probe (see k_line_probe): n_loads = 8 * threads; returns ms per launch.
+int prd_line_probe(int device, int64_t table_bytes, int64_t n_loads, int mode, int g, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  if (g < 1 || g > 16 || (mode == 1 && g > 8)) return -1;
+  void *tab = nullptr, *out = nullptr;
+  PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8));
+  const int64_t nt = n_loads / 8;
+  const uint32_t nl = (uint32_t)(table_bytes / 128);
+  const dim3 grid((unsigned)((nt + 255) / 256));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i) {
+      if (mode == 0) hipLaunchKernelGGL(k_line_probe<0>, grid, dim3(256), 0, 0, (const double *)tab, nl, nt, 977u * i, g, (double *)out);
+      else hipLaunchKernelGGL(k_line_probe<1>, grid, dim3(256), 0, 0, (const double *)tab, nl, nt, 977u * i, g, (double *)out);
     }
     PR_HIP(hipGetLastError());
     PR_HIP(hipEventRecord(b, 0));
