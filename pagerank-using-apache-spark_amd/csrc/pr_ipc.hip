@@ -399,9 +399,18 @@ struct HipIpcOps {
     PR_HIP(hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + b], 0));
     return PR_OK;
   }
-  int wait_copy(int q, int kind, int b, int c, int64_t) {
+  int wait_copy(int q, int kind, int b, int c, int64_t v) {
     if (kind != kIpcSent) return fail("IPC exchange: a copy stream only waits for sent records");
-    PR_HIP(hipStreamWaitEvent(s->cstream[q], s->peer_sent[((size_t)q * 2 + b) * s->nc + c], 0));
+    hipEvent_t e = s->peer_sent[((size_t)q * 2 + b) * s->nc + c];
+    if (!e || !s->cstream[q]) return fail("IPC exchange: a peer's sent event or a copy stream is missing");
+    const hipError_t rc = hipStreamWaitEvent(s->cstream[q], e, 0);
+    if (rc != hipSuccess) {
+      (void)hipGetLastError();
+      return pr::fail(PR_ERR_HIP, std::string("IPC exchange: wait for peer ") + std::to_string(q) + "'s sent[" +
+                                      std::to_string(b) + "] chunk " + std::to_string(c) + " of " + std::to_string(s->nc) +
+                                      " (record " + std::to_string(v) + ", early " + std::to_string(g->x_ipc_early) +
+                                      ", chunked " + std::to_string(g->x_chunked) + "): " + hipGetErrorString(rc));
+    }
     return PR_OK;
   }
   int record(int kind, int b, int c, int64_t) {

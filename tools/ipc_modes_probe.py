@@ -1,0 +1,79 @@
+"""Cycle the exchange transports of the RCCL path on a shared device and check each against RCCL.
+
+Diagnostics for the IPC transport (PR_OPT_XCHG_IPC 1 / 2 with and without chunked copies): every
+rank builds its part of an R-MAT graph, attaches the library's communicator, computes the RCCL
+unchunked reference after `--iters` iterations, then runs a fixed sequence of mode switches, each
+followed by reset + iterations, and prints per step whether its ranks equal the reference bit for
+bit (or the error the library raised).  Launch with torch.distributed.run (one GPU or several).
+
+usage: python -m torch.distributed.run --nproc-per-node 2 tools/ipc_modes_probe.py [--scale 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
+
+SEQ = [(0, 0), (1, 0), (1, 1), (2, 1), (2, 0), (0, 1), (1, 1), (2, 1), (1, 0), (2, 1), (0, 0), (2, 1), (2, 1)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--classes", type=int, default=16)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    os.environ["NCCL_HOSTID"] = f"pr-probe-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import sparky_hip
+    from sparky_hip.workloads import generate
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
+    wl = generate("rmat", scale=a.scale, device=dev)
+    V = wl.n_vertices
+    g = sparky_hip.PageRankGraph(V, wl.src.data_ptr(), wl.dst.data_ptr(), device=dev, device_input=True,
+                                 n_edges=wl.n_edges, part=rank, n_parts=world, keep_canonical=False,
+                                 options={"classes": a.classes})
+    del wl
+    obj = [sparky_hip.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    g.attach_comm(rank, world, obj[0])
+
+    def run():
+        g.reset()
+        g.step(a.iters)
+        g.sync()
+        out = np.zeros(V)
+        g.ranks(out)
+        return out
+
+    ref = None
+    for i, (ipc, chunks) in enumerate(SEQ):
+        rec = {"rank": rank, "step": i, "ipc": ipc, "chunks": chunks}
+        try:
+            g.set_exchange_ipc(ipc)
+            g.set_exchange_chunks(bool(chunks))
+            r = run()
+            if ref is None:
+                ref = r
+            rec["bitwise_equal_ref"] = bool(np.array_equal(r, ref))
+        except Exception as e:  # noqa: BLE001 -- reported per step
+            rec["error"] = str(e)
+        print(json.dumps(rec), flush=True)
+        if "error" in rec:
+            break
+    g.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

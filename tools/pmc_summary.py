@@ -86,6 +86,7 @@ def main():
         "fetch_size_kb_median": fetch[len(fetch) // 2] if fetch else None,
         "write_size_kb_median": write[len(write) // 2] if write else None,
         "bench_ms_per_step": line.get("ms_per_step"),
+        "source": os.path.relpath(os.path.abspath(d), os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")),
     }
     if hit and miss:
         h, m = hit[len(hit) // 2], miss[len(miss) // 2]
@@ -99,7 +100,9 @@ def main():
     if fp is not None and wp is not None:
         res["pass_fetch_kb"], res["pass_write_kb"] = fp, wp
         res["hbm_bytes_per_pass"] = (2 * fp + wp) * 1024
-        res["pass_kernels"] = list(PASS_KERNELS)
+        # the pass kernels this trace actually ran (e.g. k_epilogue_grp, not the k_epilogue fallback)
+        res["pass_kernels"] = sorted({r["Name"].split("(")[0].replace("void ", "").replace("pr::", "").split("<")[0]
+                                      for r in pass_stats})
     res["trace_pass_kernels"] = {r["Name"].split("(")[0]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
                                  for r in pass_stats}
     print(json.dumps(res, indent=1))

@@ -16,7 +16,24 @@ Kp is scaled so that C*Kp / V matches R-MAT s26 (64 * 18429 / 32.8 M).  Per map:
 in-link, and the per-XCD balance of LDS-served and cold entries (XCD = class % 8; the phased
 k_spmv_hot runs an XCD's classes back to back, so the slowest XCD bounds the pass).
 
-usage: python tools/sim_slots.py SCALE
+Round 5 adds the variants the round-4 sim rejected for imbalance, with the
+imbalance removed where the hardware allows it:
+
+  hot blocks, spread    the "hot blocks" map, but a segment whose in-links are all hot (LDS-served)
+                        needs no L2 residency, so its wave units may run on any XCD (in an extra
+                        phase that stages that class's hot set): only mixed and cold segments stay
+                        on their class's XCD.  Same slots as "hot blocks"; the balance is the best
+                        spread of the movable hot-only work.
+  hot/cold classes      hot block b is class b (LDS only, spreadable), cold sources round-robin over
+                        C further classes (L2-resident, pinned): a row's hot and cold in-links never
+                        share a slot.
+
+Per variant also the projected pass bytes: the slot round trip (16 B per slot: written by
+k_spmv_hot, read by the epilogue) against the measured s26 pass (profiles/pmc_spmv.json: 9.41 GB,
+277 M slots), and the XCD balance as time: per XCD, LDS entries at 1.94 T/s / 8 plus cold entries at
+268 G/s / 8 (profiles/rates.json), max over XCDs against the mean.
+
+usage: python tools/sim_slots.py SCALE [rmat|er]
 """
 import sys
 import time
@@ -43,11 +60,25 @@ def rmat(scale, ef=16, seed=2):
     return (keys >> np.uint64(32)).astype(np.int64), (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
 
 
+def er(scale, ef=16, seed=3):
+    E = ef << scale
+    rng = np.random.default_rng(seed)
+    s = rng.integers(0, 1 << scale, E, dtype=np.uint64)
+    d = rng.integers(0, 1 << scale, E, dtype=np.uint64)
+    keys = np.unique((s << np.uint64(32)) | d)
+    return (keys >> np.uint64(32)).astype(np.int64), (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
+
+
+LDS_RATE, L2_RATE = 1.94e12, 268e9  # profiles/rates.json: LDS reads, L2 gathers per second (chip)
+S26_PASS_BYTES, S26_SLOTS = 9.41e9, 277e6  # measured (profiles/pmc_spmv.json, layout stats)
+
+
 def main():
     scale = int(sys.argv[1]) if len(sys.argv) > 1 else 22
+    kind = sys.argv[2] if len(sys.argv) > 2 else "rmat"
     C = 64
     t0 = time.time()
-    src, dst = rmat(scale)
+    src, dst = rmat(scale) if kind == "rmat" else er(scale)
     nv = 1 << scale
     outdeg = np.bincount(src, minlength=nv)
     present = np.zeros(nv, bool)
@@ -62,7 +93,8 @@ def main():
     Kp = max(1, int(round(18429 * V / 32.8e6)))
     H = C * Kp
     hot = j < H
-    print(f"R-MAT s{scale}: V {V}, E' {E}, C {C}, Kp {Kp}, hot cover {hot.mean():.3f} ({time.time() - t0:.0f} s)")
+    print(f"{'R-MAT' if kind == 'rmat' else 'ER'} s{scale}: V {V}, E' {E}, C {C}, Kp {Kp}, hot cover {hot.mean():.3f} "
+          f"({time.time() - t0:.0f} s)")
 
     def report(name, cls, ncls, is_hot):
         k = np.sort(dst * ncls + cls)
@@ -74,9 +106,50 @@ def main():
               f"XCD max/mean: LDS entries {xh.max() / xh.mean():.2f}, cold {xc.max() / xc.mean():.2f}", flush=True)
         return ns
 
+    def xcd_time(cls, ncls, is_hot, movable=None):
+        """per-XCD pass-time estimate (ms at this scale): pinned work by class % 8, then the movable
+        hot-only work spread to level the XCDs as far as it goes; returns max / mean"""
+        xcd = np.arange(ncls) % 8
+        w = np.where(is_hot, 8.0 / LDS_RATE, 8.0 / L2_RATE)
+        pin = ~movable if movable is not None else np.ones(E, bool)
+        t = np.bincount(xcd[cls[pin]], weights=w[pin], minlength=8)
+        free = float(w[~pin].sum()) if movable is not None else 0.0
+        level = max(t.max(), (t.sum() + free) / 8)  # water-filling: never below the pinned maximum
+        return level / ((t.sum() + free) / 8)
+
+    def hot_only_mask(cls, ncls, is_hot):
+        """per in-link: its (row, class) segment holds hot in-links only"""
+        k = dst * ncls + cls
+        order = np.argsort(k, kind="stable")
+        ks = k[order]
+        starts = np.r_[True, ks[1:] != ks[:-1]]
+        seg = np.cumsum(starts) - 1
+        cold_in_seg = np.bincount(seg, weights=(~is_hot[order]).astype(np.float64))
+        m = np.empty(E, bool)
+        m[order] = cold_in_seg[seg] == 0
+        return m
+
+    def bytes_note(ns, base):
+        saved = (base - ns) * 16.0 * (S26_SLOTS / base)  # scaled to s26's slot count
+        return f"projected s26 pass bytes {1 - saved / S26_PASS_BYTES:.1%} of today's ({saved / 1e9:.2f} GB less)"
+
     base = report("round-robin", j % C, C, hot)
-    blk = report("hot blocks", np.where(hot, j // Kp, (j - H) % C), C, hot)
-    print(f"  hot blocks: {1 - blk / base:.1%} fewer slots")
+    print(f"  XCD time max/mean {xcd_time(j % C, C, hot):.3f}")
+    cls_b = np.where(hot, j // Kp, (j - H) % C)
+    blk = report("hot blocks", cls_b, C, hot)
+    print(f"  hot blocks: {1 - blk / base:.1%} fewer slots; {bytes_note(blk, base)}")
+    print(f"  pinned: XCD time max/mean {xcd_time(cls_b, C, hot):.3f}")
+    mov = hot_only_mask(cls_b, C, hot)
+    print(f"  spread (hot-only segments movable, {mov.mean():.1%} of in-links): XCD time max/mean "
+          f"{xcd_time(cls_b, C, hot, mov):.3f}", flush=True)
+    cls_hc = np.where(hot, j // Kp, C + (j - H) % C)
+    hc = report("hot/cold cls", cls_hc, 2 * C, hot)
+    print(f"  hot/cold classes: {1 - hc / base:.1%} fewer slots; {bytes_note(hc, base)}; XCD time max/mean "
+          f"{xcd_time(cls_hc, 2 * C, hot, hot):.3f}", flush=True)
+    if kind == "er":
+        for c2 in (32, 16):
+            ns = report(f"round-robin {c2}", j % c2, c2, j < c2 * Kp)
+            print(f"  {c2} classes: {1 - ns / base:.1%} fewer slots (class regions {64 // c2}x larger)")
     for nh in (1, 2, 4):
         hub = j < nh * Kp
         cls = np.where(hub, C + j // Kp, (j - nh * Kp) % C)
