@@ -45,6 +45,16 @@ namespace pr {
 
 enum IpcKind { kIpcSent = 0, kIpcCopied = 1 };
 
+// Per-chunk publication: the epilogue groups (of rows_per_grp local rows) launched before chunk c's
+// record.  Chunk c of the send runs holds the sources at local rows below (c + 1) * chunk_rows (the
+// class regions of hot phase c); launch c covers groups [end(c - 1), end(c)), so every row of chunk
+// c is written before its record and the launches partition [0, ngrp).
+inline int64_t ipc_epi_chunk_end(int64_t ngrp, int c, int nxc, int64_t chunk_rows, int64_t rows_per_grp) {
+  if (c >= nxc - 1) return ngrp;
+  const int64_t e = ((int64_t)(c + 1) * chunk_rows + rows_per_grp - 1) / rows_per_grp;
+  return e < ngrp ? e : ngrp;
+}
+
 template <class Ops>
 struct IpcProtocol {
   int P = 0, self = 0;

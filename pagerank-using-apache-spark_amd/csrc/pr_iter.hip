@@ -27,6 +27,7 @@
 
 #include "pr_device.h"
 #include "pr_graph.h"
+#include "pr_ipc_protocol.h"
 #include "pr_spmv.h"
 
 namespace pr {
@@ -400,8 +401,7 @@ int iter_compute(pr_graph *g) {
       const int wpb = epi_grp_threads(g->epi_narrow) / kWave;
       int64_t g_lo = 0;
       for (int c = 0; c < g->n_xc; ++c) {
-        const int64_t g_hi = c == g->n_xc - 1 ? ngrp
-                                               : std::min(ngrp, ((int64_t)(c + 1) * chunk_rows + rows_per_grp - 1) / rows_per_grp);
+        const int64_t g_hi = ipc_epi_chunk_end(ngrp, c, g->n_xc, chunk_rows, rows_per_grp);
         if (g_hi > g_lo) PR_TRY(epilogue(g_lo, g_hi, grid_for(g_hi - g_lo, wpb, 1u << 20)));
         g_lo = std::max(g_lo, g_hi);
         if (c < g->n_xc - 1) PR_TRY(ipc_chunk_sent(g, out, c));

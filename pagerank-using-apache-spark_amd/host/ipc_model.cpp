@@ -2,7 +2,7 @@
 // template the library runs (csrc/pr_ipc.hip).  One thread per rank runs a seeded sequence of
 // resets and iterations -- the same sequence on every rank, as the library requires -- with random
 // delays; interprocess events are modelled as "the number of records enqueued so far" per (rank,
-// kind, buffer), and the record counters as atomics.  Every stream wait checks that the latest
+// kind, buffer, chunk), and the record counters as atomics.  Every stream wait checks that the latest
 // record of the peer's event at that moment is exactly the record the protocol means (so the
 // device wait would bind to it), and the run ends without deadlock.  Used by
 // tests/test_ipc_protocol_cpu.py through ipc_model_run().
@@ -124,6 +124,11 @@ struct ModelOps {
 }  // namespace
 
 extern "C" {
+
+// pr_ipc_protocol.h ipc_epi_chunk_end, for tests/test_ipc_protocol_cpu.py
+int64_t ipc_model_chunk_end(int64_t ngrp, int c, int nxc, int64_t chunk_rows, int64_t rows_per_grp) {
+  return pr::ipc_epi_chunk_end(ngrp, c, nxc, chunk_rows, rows_per_grp);
+}
 
 // P ranks, nc sent chunks per buffer, run n_ops steps each (seeded, the same sequence on every
 // rank: 0 = reset, which writes and exchanges buffer 0 with the pack kernel; otherwise an

@@ -28,6 +28,8 @@ def model():
     lib.ipc_model_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                   ctypes.c_char_p, ctypes.c_int]
     lib.ipc_model_run.restype = ctypes.c_int64
+    lib.ipc_model_chunk_end.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+    lib.ipc_model_chunk_end.restype = ctypes.c_int64
     return lib
 
 
@@ -57,3 +59,25 @@ def test_the_model_catches_a_broken_order(model):
     err = ctypes.create_string_buffer(512)
     caught = any(model.ipc_model_run(4, 8, 200, s, -30, err, len(err)) < 0 for s in range(1, 6))
     assert caught and b"latest record" in err.value
+
+
+@pytest.mark.parametrize("C,Q_pad", [(16, 4096), (32, 5120), (64, 512 * 1024 + 64), (64, 64), (128, 1 << 20), (64, 8000)])
+def test_epilogue_chunk_launches_cover_each_chunk_before_its_record(model, C, Q_pad):
+    """PR_OPT_XCHG_IPC = 2 (pr_iter.hip): the epilogue launch before chunk c's record covers every
+    group holding a row of chunks <= c (local rows below (c + 1) * 8 * Q_pad), and the launches
+    partition the groups (each row's update runs exactly once)."""
+    import numpy as np
+
+    nxc, rows_per_grp = C // 8, 8 * 64
+    n_rows = C * Q_pad
+    ngrp = (n_rows + rows_per_grp - 1) // rows_per_grp
+    ends = [model.ipc_model_chunk_end(ngrp, c, nxc, 8 * Q_pad, rows_per_grp) for c in range(nxc)]
+    assert ends[-1] == ngrp and all(a <= b for a, b in zip(ends, ends[1:]))
+    covered = np.zeros(ngrp, np.int32)
+    lo = 0
+    for c, hi in enumerate(ends):
+        covered[lo:hi] += 1
+        last_row_of_chunk = min((c + 1) * 8 * Q_pad, n_rows) - 1
+        assert last_row_of_chunk // rows_per_grp < hi  # its group ran before the record
+        lo = max(lo, hi)
+    assert (covered == 1).all()
