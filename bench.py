@@ -238,10 +238,14 @@ def parity_failures(parity) -> list:
         elif (k.endswith("bitwise_equal_rccl") or k in ("csr_bit_exact", "every_row_owned_once")) and v is False:
             bad.append(f"{k} is false")
     for name, rec in (parity.get("modes") or {}).items():
+        if rec.get("error"):
+            bad.append(f"mode {name} failed: {rec['error']}")
+            continue
         if not rec.get("bitwise_equal_rccl_unchunked", True):
             bad.append(f"mode {name} not bitwise equal to RCCL unchunked")
-        if not (rec.get("max_rel", 0.0) <= RANK_TOL):
-            bad.append(f"mode {name} max_rel {rec['max_rel']:.3e}")
+        mr = rec.get("max_rel", 0.0)
+        if mr is None or not (mr <= RANK_TOL):
+            bad.append(f"mode {name} max_rel {mr}")
     return bad
 
 
@@ -602,14 +606,28 @@ def main() -> int:
     if validate:
         K = a.parity_iters
 
+        def agree_all(ok: bool) -> bool:
+            if dist is None:
+                return ok
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return bool(t.item())
+
         def gpu_ranks():
             """K iterations from a fresh reset in the current mode: (this rank's rows, every rank's rows
-            summed on rank 0, every row owned exactly once)."""
-            g.reset()
-            g.step(K)
-            g.sync()
+            summed on rank 0, every row owned exactly once).  A failure on any rank is agreed before the
+            reductions (so no rank waits in one alone) and raised on every rank."""
             mine = np.zeros(V, np.float64)
-            g.ranks(mine)  # this rank's rows; the others stay 0
+            err = None
+            try:
+                g.reset()
+                g.step(K)
+                g.sync()
+                g.ranks(mine)  # this rank's rows; the others stay 0
+            except Exception as e:  # noqa: BLE001 -- agreed below
+                err = e
+            if not agree_all(err is None):
+                raise RuntimeError(f"parity run failed on a rank: {err or 'a peer failed'}")
             merged, owned_once = mine, True
             if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
                 rt = torch.from_numpy(mine).cuda()
@@ -643,13 +661,24 @@ def main() -> int:
         set_mode(ref_mode)
         ref_local, mine, owned_once = gpu_ranks()
         checked = {}  # name -> (merged ranks on rank 0, bitwise equal to the reference on every rank)
+        failed = {}
         if overlap is not None:
             others = [mode] + [m for m in [EXCHANGE_MODES[1]] + IPC_MODES if m[0] != mode[0] and (ipc_ok or not m[3])]
+            failed = {}
             for m in others:
                 if m[0] == ref_mode[0]:
                     continue
-                set_mode(m)
-                loc, merged, oc = gpu_ranks()
+                try:
+                    set_mode(m)
+                    loc, merged, oc = gpu_ranks()
+                except Exception as e:  # noqa: BLE001 -- a mode that cannot run fails the parity check
+                    failed[m[0]] = str(e)
+                    log(f"parity run of mode {m[0]} failed: {e}")
+                    try:
+                        set_mode(ref_mode)
+                    except Exception as e2:  # noqa: BLE001
+                        raise RuntimeError(f"mode {m[0]} failed ({e}) and the switch back to RCCL failed ({e2})")
+                    continue
                 owned_once = owned_once and oc
                 checked[m[0]] = (merged if rank == 0 else None, all_ranks_equal(loc, ref_local))
                 del loc
@@ -669,7 +698,11 @@ def main() -> int:
                 if world > 1:
                     parity["max_rel_timed_mode"] = parity["max_rel"]
                     parity["timed_mode_bitwise_equal_rccl"] = True
-                per_mode = {}
+                per_mode = {name: {"max_rel": None, "bitwise_equal_rccl_unchunked": False, "error": err}
+                            for name, err in failed.items()}
+                if mode[0] in failed:
+                    parity["max_rel_timed_mode"] = None
+                    parity["timed_mode_bitwise_equal_rccl"] = False
                 for name, (merged, same_bits) in checked.items():
                     mr = float(np.max(np.abs(merged - ref) / ref)) if V else 0.0
                     per_mode[name] = {"max_rel": mr, "bitwise_equal_rccl_unchunked": same_bits}
