@@ -430,6 +430,7 @@ struct HipIpcOps {
   int fail(const char *msg) { return pr::fail(PR_ERR_STATE, msg); }
 
   int copy_steps() const { return g->x_chunked ? s->nc : 1; }
+  bool per_chunk() const { return g->x_ipc_early; }
   // the transfer stream joins this rank's pass (timing: pack done -> last chunk in); every copy
   // stream waits only until this rank no longer reads gather buffer b (x_free_ev, recorded before
   // the pass), so a peer's chunk can land while this rank's own epilogue still runs

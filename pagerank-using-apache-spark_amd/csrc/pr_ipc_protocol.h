@@ -32,6 +32,10 @@
 //                                  stream, copied: transfer stream)
 //   publish(kind, b, k)            make this rank's k-th records of kind[b] visible to the peers
 //   pack(b)                        write the runs of b (when the pass did not: pack kernel)
+//   per_chunk()                    the pass publishes chunk by chunk (PR_OPT_XCHG_IPC = 2): every
+//                                  chunk has its own record; otherwise only the last chunk's event is
+//                                  recorded and every copy waits for it (one record per exchange, the
+//                                  round-4 transport)
 //   copy_steps()                   how many steps the copies take (1: whole runs; nc: per chunk)
 //   copy_begin(b)                  the copy streams wait until this rank's gather buffer b is free
 //   copy(q, b, lo, hi)             copy chunks [lo, hi) of peer q's run of b
@@ -86,6 +90,7 @@ struct IpcProtocol {
   // During the pass (fused pack): the runs of chunk c of b are written; chunks in order, c < nc - 1
   // (the last chunk carries the two slots k_finalize writes, recorded by exchange()).
   int chunk_sent(Ops &o, int b, int c) {
+    if (!o.per_chunk()) return o.fail("IPC exchange: chunk records without per-chunk publication");
     const int64_t k = n[b] + 1;
     if (freed[b] < k) return o.fail("IPC exchange: chunk recorded before the reuse wait");
     if (c != rec_c[b] || c >= nc - 1) return o.fail("IPC exchange: chunk records out of order");
@@ -104,7 +109,8 @@ struct IpcProtocol {
     }
     const int64_t k = ++n[b];
     if (freed[b] < k) return o.fail("IPC exchange: send runs written without the reuse wait");
-    for (int c = rec_c[b]; c < nc; ++c)
+    const bool pc = o.per_chunk();
+    for (int c = pc ? rec_c[b] : nc - 1; c < nc; ++c)
       if ((rv = o.record(kIpcSent, b, c, k)) != 0) return rv;
     rec_c[b] = 0;
     if ((rv = o.publish(kIpcSent, b, k)) != 0) return rv;
@@ -119,7 +125,7 @@ struct IpcProtocol {
       const int lo = steps == 1 ? 0 : s, hi = steps == 1 ? nc : s + 1;
       for (int q = 0; q < P; ++q) {
         if (q == self) continue;
-        if ((rv = o.wait_copy(q, kIpcSent, b, hi - 1, k)) != 0) return rv;
+        if ((rv = o.wait_copy(q, kIpcSent, b, pc ? hi - 1 : nc - 1, k)) != 0) return rv;
         if ((rv = o.copy(q, b, lo, hi)) != 0) return rv;
       }
       if ((rv = o.step_done(lo, hi)) != 0) return rv;

@@ -1,8 +1,8 @@
 // CPU model checker of the IPC exchange's host-side ordering (csrc/pr_ipc_protocol.h), the same
 // template the library runs (csrc/pr_ipc.hip).  One thread per rank runs a seeded sequence of
 // resets and iterations -- the same sequence on every rank, as the library requires -- with random
-// delays; interprocess events are modelled as "the number of records enqueued so far" per (rank,
-// kind, buffer, chunk), and the record counters as atomics.  Every stream wait checks that the latest
+// delays; interprocess events are modelled as "the exchange of the latest record enqueued so far"
+// per (rank, kind, buffer, chunk), and the record counters as atomics.  Every stream wait checks that the latest
 // record of the peer's event at that moment is exactly the record the protocol means (so the
 // device wait would bind to it), and the run ends without deadlock.  Used by
 // tests/test_ipc_protocol_cpu.py through ipc_model_run().
@@ -53,6 +53,7 @@ struct ModelOps {
   int max_delay_us;
   bool broken;     // checker self-test: no host spin before the sent waits
   int steps = 1;   // copy steps of the current exchange (1: whole runs; nc: per chunk)
+  bool pc = false;  // per-chunk publication (every chunk its own record)
 
   void delay() {
     if (max_delay_us <= 0) return;
@@ -90,16 +91,18 @@ struct ModelOps {
   int wait_compute(int q, int kind, int b, int c, int64_t v) { return wait_any(q, kind, b, c, v); }
   int wait_copy(int q, int kind, int b, int c, int64_t v) { return wait_any(q, kind, b, c, v); }
   int record(int kind, int b, int c, int64_t k) {
-    const int64_t e = w->enq[w->ex(self, kind, b, c)].fetch_add(1) + 1;
-    if (e != k)
-      return w->fail("rank " + std::to_string(self) + " enqueued record " + std::to_string(e) + " of chunk " +
-                     std::to_string(c) + " as " + std::to_string(k));
+    // the event's latest record is now exchange k's (a chunk may skip exchanges whose sender
+    // published whole runs, so the value is the exchange number, not a count)
+    const int64_t prev = w->enq[w->ex(self, kind, b, c)].exchange(k);
+    if (prev >= k)
+      return w->fail("rank " + std::to_string(self) + " recorded chunk " + std::to_string(c) + " for exchange " +
+                     std::to_string(k) + " after exchange " + std::to_string(prev));
     delay();
     return 0;
   }
   int publish(int kind, int b, int64_t k) {
     const int n = kind == pr::kIpcSent ? w->nc : 1;
-    for (int c = 0; c < n; ++c)  // every chunk's record k is enqueued before k is published
+    for (int c = (kind == pr::kIpcSent && !pc) ? n - 1 : 0; c < n; ++c)  // record k enqueued before k is published
       if (w->enq[w->ex(self, kind, b, c)].load() != k)
         return w->fail("rank " + std::to_string(self) + " published " + std::to_string(k) + " before chunk " +
                        std::to_string(c) + "'s record");
@@ -112,6 +115,7 @@ struct ModelOps {
     return 0;
   }
   int copy_steps() const { return steps; }
+  bool per_chunk() const { return pc; }
   int copy_begin(int) { return 0; }
   int copy(int, int, int, int) {
     delay();
@@ -158,6 +162,9 @@ int64_t ipc_model_run(int P, int nc, int n_ops, uint64_t seed, int max_delay_us,
       for (size_t i = 0; i < ops.size(); ++i) {
         const int op = ops[i];
         o.steps = steps[i];
+        // per-chunk publication is a mode (PR_OPT_XCHG_IPC = 2): the same on every rank; a reset
+        // exchanges with the pack kernel either way
+        o.pc = op == 0 ? (steps[i] & 1) != 0 : op >= 5;
         if (w.failed.load()) return;
         int rv;
         if (op == 0) {  // pr_reset: k_finalize writes the slots of buffer 0's runs, then exchange(0)

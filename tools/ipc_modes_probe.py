@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--scale", type=int, default=20)
     ap.add_argument("--classes", type=int, default=16)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the switch sequence")
+    ap.add_argument("--only", type=int, default=-1, help="run only this IPC mode (with chunks on), after the reference")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"pr-probe-rank{rank}"
@@ -57,7 +59,9 @@ def main():
         return out
 
     ref = None
-    for i, (ipc, chunks) in enumerate(SEQ):
+    seq = SEQ * a.rounds if a.only < 0 else [(0, 0)] + [(a.only, 1)] * (len(SEQ) * a.rounds)
+    n_err = 0
+    for i, (ipc, chunks) in enumerate(seq):
         rec = {"rank": rank, "step": i, "ipc": ipc, "chunks": chunks}
         try:
             g.set_exchange_ipc(ipc)
@@ -70,7 +74,13 @@ def main():
             rec["error"] = str(e)
         print(json.dumps(rec), flush=True)
         if "error" in rec:
-            break
+            n_err += 1
+            try:  # back to RCCL together (every rank raised: the failure is agreed by the library's spins)
+                g.set_exchange_ipc(0)
+            except Exception as e:  # noqa: BLE001
+                print(json.dumps({"rank": rank, "switch_back_error": str(e)}), flush=True)
+                break
+    print(json.dumps({"rank": rank, "steps": len(seq), "errors": n_err}), flush=True)
     g.close()
     dist.destroy_process_group()
 
