@@ -28,9 +28,18 @@
 //            one exchange apart per buffer, so a later record of the same event cannot be taken for
 //            the one meant (its owner would first have had to pass a wait on this rank).  A host
 //            spin that exceeds kSpinLimit fails with PR_ERR_COMM instead of hanging.
-// Set-up and switching are collective (pr_set_option on every rank): handles and page names travel
-// by ncclAllGather over the attached communicator, and every rank agrees on success with an
-// ncclAllReduce before the mode is used.
+//   events   the HIP runtime's interprocess events take at most 32 records each (their
+//            shared-memory ring of signals; measured: the 33rd record's wait fails with "invalid
+//            argument" and the event stays broken, profiles/r05/ipc_events/), so every event here is
+//            recorded at most kRecordsPerEvent times and then replaced by a fresh one: its owner
+//            writes the new handle into one of three slots per event of its shared-memory page,
+//            stamped with the first exchange it serves, before it publishes that exchange; a waiter
+//            that needs exchange k picks the newest slot whose range holds k and opens that handle
+//            once.  An event is replaced three generations after it was last meant, long after
+//            every wait on it (the hosts stay within one exchange per buffer of each other).
+// Set-up and switching are collective (pr_set_option on every rank): the memory handle, run offsets
+// and page names travel by ncclAllGather over the attached communicator, and every rank agrees on
+// success with an ncclAllReduce before the mode is used.
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <time.h>
@@ -59,18 +68,28 @@ namespace {
 constexpr double kSpinLimit = 120.0;  // seconds a host waits for a peer's record before failing
 constexpr int kIpcMaxChunks = 16;     // sent events per buffer: one per exchange chunk (C / 8 <= 16)
 
-// one rank's shared-memory page: how many sent[b] / copied[b] records it has enqueued
+constexpr int64_t kRecordsPerEvent = 30;  // below the runtime's 32-record ring (see "events" above)
+constexpr int kGens = 3;                  // handle slots per event in the page
+
+// one generation of one event: the exchanges [first_k, first_k + kRecordsPerEvent) it serves
+struct IpcSlot {
+  std::atomic<int64_t> id;       // generation id (0: empty), stored last (release)
+  std::atomic<int64_t> first_k;
+  hipIpcEventHandle_t h;
+};
+
+// one rank's shared-memory page: how many sent[b] / copied[b] records it has enqueued, and the
+// handles of its events, per (kind, buffer, chunk) three generations
 struct alignas(64) IpcCounters {
   std::atomic<int64_t> sent[2];
   std::atomic<int64_t> copied[2];
+  IpcSlot slot[2][2][kIpcMaxChunks][kGens];  // [kind][b][c][generation % kGens]
 };
 static_assert(std::atomic<int64_t>::is_always_lock_free, "cross-process counters must be lock-free");
 
 // what every rank publishes at set-up (ncclAllGather of bytes)
 struct IpcRecord {
   hipIpcMemHandle_t mem;         // its x_sbuf
-  hipIpcEventHandle_t sent[2][kIpcMaxChunks];  // its sent[b] per chunk
-  hipIpcEventHandle_t copied[2];  // its copied[b]
   char page[64];                 // its counter page (shm_open name)
   int64_t stride;                // doubles per send buffer (send_stride)
   int64_t soff[kMaxParts + 1];   // its send-run offsets
@@ -90,10 +109,21 @@ struct IpcState {
   std::vector<void *> peer_sbuf;      // mapped send buffers
   std::vector<int64_t> peer_stride;   // doubles per peer send buffer
   std::vector<int64_t> peer_soff_me;  // start of the peer's run for this rank
-  std::vector<hipEvent_t> sent;  // [b * nc + c]
-  hipEvent_t copied[2] = {nullptr, nullptr};
-  std::vector<hipEvent_t> peer_sent;    // [(q * 2 + b) * nc + c]
-  std::vector<hipEvent_t> peer_copied;  // [q * 2 + b]
+  // own events per (kind, b, c) and generation slot, with the slot's id / first exchange; the
+  // current slot per (kind, b, c) (-1: none yet); the next generation id
+  struct Own {
+    hipEvent_t ev[kGens] = {nullptr, nullptr, nullptr};
+    int64_t first_k[kGens] = {0, 0, 0};
+    int cur = -1;
+  };
+  std::vector<Own> own;  // [(kind * 2 + b) * nc + c]
+  int64_t next_id = 1;
+  // the peers' events as opened here, per (q, kind, b, c) and slot: the generation id it holds
+  struct Opened {
+    hipEvent_t ev[kGens] = {nullptr, nullptr, nullptr};
+    int64_t id[kGens] = {0, 0, 0};
+  };
+  std::vector<Opened> opened;  // [((q * 2 + kind) * 2 + b) * nc + c]
   // one copy stream per peer, so the runs of different peers move at once (on their own copy
   // engines / xGMI links), and per (peer, chunk) the event the transfer stream joins on
   std::vector<hipStream_t> cstream;
@@ -138,14 +168,12 @@ void free_state(IpcState *s) {
     if (e) (void)hipEventDestroy(e);
   for (size_t q = 0; q < s->peer_sbuf.size(); ++q)
     if (s->peer_sbuf[q]) (void)hipIpcCloseMemHandle(s->peer_sbuf[q]);
-  for (hipEvent_t e : s->peer_sent)
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : s->peer_copied)
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : s->sent)
-    if (e) (void)hipEventDestroy(e);
-  for (int b = 0; b < 2; ++b)
-    if (s->copied[b]) (void)hipEventDestroy(s->copied[b]);
+  for (auto &o : s->opened)
+    for (hipEvent_t e : o.ev)
+      if (e) (void)hipEventDestroy(e);
+  for (auto &o : s->own)
+    for (hipEvent_t e : o.ev)
+      if (e) (void)hipEventDestroy(e);
   for (IpcCounters *c : s->peer) unmap_page(c);
   if (s->mine) {
     unmap_page(s->mine);
@@ -239,9 +267,8 @@ int ipc_setup(pr_graph *g) {
   s->peer_soff_me.assign(P, 0);
   s->nc = g->n_xc;
   s->proto.nc = s->nc;
-  s->sent.assign(2 * (size_t)s->nc, nullptr);
-  s->peer_sent.assign(2 * (size_t)P * s->nc, nullptr);
-  s->peer_copied.assign(2 * (size_t)P, nullptr);
+  s->own.assign(4 * (size_t)s->nc, IpcState::Own{});
+  s->opened.assign(4 * (size_t)P * s->nc, IpcState::Opened{});
   s->cstream.assign(P, nullptr);
   s->cev.assign((size_t)P * s->nc, nullptr);
   local(s->nc >= 1 && s->nc <= kIpcMaxChunks, "exchange chunk count out of range");
@@ -253,17 +280,6 @@ int ipc_setup(pr_graph *g) {
     std::memcpy(rec.page, s->page, sizeof(rec.page));
   }
   if (rec.ok) local(hipIpcGetMemHandle(&rec.mem, g->x_sbuf.p) == hipSuccess, "hipIpcGetMemHandle failed");
-  for (int b = 0; b < 2 && rec.ok; ++b) {
-    local(hipEventCreateWithFlags(&s->copied[b], hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
-          "hipEventCreateWithFlags(hipEventInterprocess) failed");
-    if (rec.ok) local(hipIpcGetEventHandle(&rec.copied[b], s->copied[b]) == hipSuccess, "hipIpcGetEventHandle failed");
-    for (int c = 0; c < s->nc && rec.ok; ++c) {
-      hipEvent_t &e = s->sent[(size_t)b * s->nc + c];
-      local(hipEventCreateWithFlags(&e, hipEventInterprocess | hipEventDisableTiming) == hipSuccess,
-            "hipEventCreateWithFlags(hipEventInterprocess) failed");
-      if (rec.ok) local(hipIpcGetEventHandle(&rec.sent[b][c], e) == hipSuccess, "hipIpcGetEventHandle failed");
-    }
-  }
   rec.stride = send_stride(g);
   for (int q = 0; q <= P; ++q) rec.soff[q] = g->x_soff[q];
   // publish (the scratch holds P + 1 records: this rank's, then everyone's)
@@ -299,19 +315,6 @@ int ipc_setup(pr_graph *g) {
       ok = 0;
       why = "hipIpcOpenMemHandle failed";
       break;
-    }
-    for (int b = 0; b < 2 && ok; ++b) {
-      if (hipIpcOpenEventHandle(&s->peer_copied[2 * q + b], r.copied[b]) != hipSuccess) {
-        (void)hipGetLastError();
-        ok = 0;
-        why = "hipIpcOpenEventHandle failed";
-      }
-      for (int c = 0; c < s->nc && ok; ++c)
-        if (hipIpcOpenEventHandle(&s->peer_sent[((size_t)q * 2 + b) * s->nc + c], r.sent[b][c]) != hipSuccess) {
-          (void)hipGetLastError();
-          ok = 0;
-          why = "hipIpcOpenEventHandle failed";
-        }
     }
     if (ok && hipStreamCreateWithFlags(&s->cstream[q], hipStreamNonBlocking) != hipSuccess) {
       (void)hipGetLastError();
@@ -394,15 +397,48 @@ struct HipIpcOps {
     const std::atomic<int64_t> &c = kind == kIpcSent ? s->peer[q]->sent[b] : s->peer[q]->copied[b];
     return spin_until(c, v, kind == kIpcSent ? "sent" : "copied", q);
   }
-  int wait_compute(int q, int kind, int b, int, int64_t) {
+  // peer q's event of (kind, b, c) that holds its record of exchange k: the newest page slot whose
+  // range holds k (written before k was published), opened here once per generation
+  int peer_event(int q, int kind, int b, int c, int64_t k, hipEvent_t *out) {
+    IpcState::Opened &o = s->opened[(((size_t)q * 2 + kind) * 2 + b) * s->nc + c];
+    int best = -1;
+    int64_t best_id = 0;
+    for (int i = 0; i < kGens; ++i) {
+      const IpcSlot &sl = s->peer[q]->slot[kind][b][c][i];
+      const int64_t id = sl.id.load(std::memory_order_acquire);
+      const int64_t f = sl.first_k.load(std::memory_order_acquire);
+      if (id > best_id && f <= k && k < f + kRecordsPerEvent) {
+        best = i;
+        best_id = id;
+      }
+    }
+    if (best < 0)
+      return pr::fail(PR_ERR_COMM, "IPC exchange: peer " + std::to_string(q) + " published exchange " + std::to_string(k) +
+                                       " without an event for it");
+    if (o.id[best] != best_id) {
+      if (o.ev[best]) (void)hipEventDestroy(o.ev[best]);
+      o.ev[best] = nullptr;
+      o.id[best] = 0;
+      hipIpcEventHandle_t h;
+      std::memcpy(&h, &s->peer[q]->slot[kind][b][c][best].h, sizeof(h));
+      PR_HIP(hipIpcOpenEventHandle(&o.ev[best], h));
+      o.id[best] = best_id;
+    }
+    *out = o.ev[best];
+    return PR_OK;
+  }
+  int wait_compute(int q, int kind, int b, int, int64_t v) {
     if (kind != kIpcCopied) return fail("IPC exchange: the compute stream only waits for copied records");
-    PR_HIP(hipStreamWaitEvent(g->stream, s->peer_copied[2 * q + b], 0));
+    hipEvent_t e = nullptr;
+    PR_TRY(peer_event(q, kIpcCopied, b, 0, v, &e));
+    PR_HIP(hipStreamWaitEvent(g->stream, e, 0));
     return PR_OK;
   }
   int wait_copy(int q, int kind, int b, int c, int64_t v) {
     if (kind != kIpcSent) return fail("IPC exchange: a copy stream only waits for sent records");
-    hipEvent_t e = s->peer_sent[((size_t)q * 2 + b) * s->nc + c];
-    if (!e || !s->cstream[q]) return fail("IPC exchange: a peer's sent event or a copy stream is missing");
+    hipEvent_t e = nullptr;
+    PR_TRY(peer_event(q, kIpcSent, b, c, v, &e));
+    if (!s->cstream[q]) return fail("IPC exchange: a copy stream is missing");
     const hipError_t rc = hipStreamWaitEvent(s->cstream[q], e, 0);
     if (rc != hipSuccess) {
       (void)hipGetLastError();
@@ -413,12 +449,37 @@ struct HipIpcOps {
     }
     return PR_OK;
   }
-  int record(int kind, int b, int c, int64_t) {
+  // this rank's event of (kind, b, c) for its record of exchange k: a fresh generation once the
+  // current one has served kRecordsPerEvent exchanges (or the counts restarted), its handle written
+  // to the page slot before k is published
+  int own_event(int kind, int b, int c, int64_t k, hipEvent_t *out) {
+    IpcState::Own &o = s->own[((size_t)kind * 2 + b) * s->nc + c];
+    if (o.cur < 0 || k < o.first_k[o.cur] || k >= o.first_k[o.cur] + kRecordsPerEvent) {
+      const int i = (o.cur + 1) % kGens;
+      IpcSlot &sl = s->mine->slot[kind][b][c][i];
+      sl.id.store(0, std::memory_order_release);  // the slot's previous generation (three back) is over
+      if (o.ev[i]) (void)hipEventDestroy(o.ev[i]);
+      o.ev[i] = nullptr;
+      PR_HIP(hipEventCreateWithFlags(&o.ev[i], hipEventInterprocess | hipEventDisableTiming));
+      hipIpcEventHandle_t h;
+      PR_HIP(hipIpcGetEventHandle(&h, o.ev[i]));
+      std::memcpy(&sl.h, &h, sizeof(h));
+      sl.first_k.store(k, std::memory_order_release);
+      sl.id.store(s->next_id++, std::memory_order_release);
+      o.first_k[i] = k;
+      o.cur = i;
+    }
+    *out = o.ev[o.cur];
+    return PR_OK;
+  }
+  int record(int kind, int b, int c, int64_t k) {
+    hipEvent_t e = nullptr;
+    PR_TRY(own_event(kind, b, c, k, &e));
     if (kind == kIpcSent) {  // chunk c of the runs of b is written (compute stream)
       if (c == s->nc - 1) PR_HIP(hipEventRecord(g->x_pack_ev, g->stream));  // the whole pass (+ pack) is done
-      PR_HIP(hipEventRecord(s->sent[(size_t)b * s->nc + c], g->stream));
+      PR_HIP(hipEventRecord(e, g->stream));
     } else {  // the transfer stream has joined every copy of b
-      PR_HIP(hipEventRecord(s->copied[b], g->xstream));
+      PR_HIP(hipEventRecord(e, g->xstream));
     }
     return PR_OK;
   }
@@ -514,8 +575,12 @@ void ipc_destroy(pr_graph *g) {
       const int64_t k = s->mine->sent[b].load(std::memory_order_acquire);
       if (k <= 0) continue;
       if (spin_until(s->peer[q]->copied[b], k, "copied", q, 10.0) != PR_OK) break;  // peer gone
+      // then its copies of exchange k (the event it recorded after them), polled with a deadline
+      hipEvent_t e = nullptr;
+      HipIpcOps o{g, s, nullptr};
+      if (o.peer_event(q, kIpcCopied, b, 0, k, &e) != PR_OK) break;
       const auto t0 = std::chrono::steady_clock::now();
-      while (hipEventQuery(s->peer_copied[2 * q + b]) == hipErrorNotReady &&
+      while (hipEventQuery(e) == hipErrorNotReady &&
              std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < 10.0)
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }

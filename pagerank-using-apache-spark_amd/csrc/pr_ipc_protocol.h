@@ -125,7 +125,10 @@ struct IpcProtocol {
       const int lo = steps == 1 ? 0 : s, hi = steps == 1 ? nc : s + 1;
       for (int q = 0; q < P; ++q) {
         if (q == self) continue;
-        if ((rv = o.wait_copy(q, kIpcSent, b, pc ? hi - 1 : nc - 1, k)) != 0) return rv;
+        // per chunk: wait for that chunk's record; otherwise one wait per exchange and peer, for the
+        // only record there is, before the first copy (each record is waited on once per peer)
+        if (pc || s == 0)
+          if ((rv = o.wait_copy(q, kIpcSent, b, pc ? hi - 1 : nc - 1, k)) != 0) return rv;
         if ((rv = o.copy(q, b, lo, hi)) != 0) return rv;
       }
       if ((rv = o.step_done(lo, hi)) != 0) return rv;
