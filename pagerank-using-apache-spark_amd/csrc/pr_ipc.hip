@@ -114,10 +114,12 @@ struct IpcState {
   struct Own {
     hipEvent_t ev[kGens] = {nullptr, nullptr, nullptr};
     int64_t first_k[kGens] = {0, 0, 0};
+    int64_t epoch = -1;  // of the current generation
     int cur = -1;
   };
   std::vector<Own> own;  // [(kind * 2 + b) * nc + c]
   int64_t next_id = 1;
+  int64_t epoch = 0;  // bumped at every enable: the exchange counts restart, so do the generations
   // the peers' events as opened here, per (q, kind, b, c) and slot: the generation id it holds
   struct Opened {
     hipEvent_t ev[kGens] = {nullptr, nullptr, nullptr};
@@ -378,6 +380,7 @@ int set_exchange_ipc(pr_graph *g, int mode) {
       s->mine->copied[b].store(0, std::memory_order_release);
     }
     s->proto.reset();
+    ++s->epoch;  // the counts restart at 1: every event starts a fresh generation
   }
   PR_TRY(comm_barrier(g, &one));
   g->x_ipc = on;
@@ -454,7 +457,7 @@ struct HipIpcOps {
   // to the page slot before k is published
   int own_event(int kind, int b, int c, int64_t k, hipEvent_t *out) {
     IpcState::Own &o = s->own[((size_t)kind * 2 + b) * s->nc + c];
-    if (o.cur < 0 || k < o.first_k[o.cur] || k >= o.first_k[o.cur] + kRecordsPerEvent) {
+    if (o.cur < 0 || o.epoch != s->epoch || k < o.first_k[o.cur] || k >= o.first_k[o.cur] + kRecordsPerEvent) {
       const int i = (o.cur + 1) % kGens;
       IpcSlot &sl = s->mine->slot[kind][b][c][i];
       sl.id.store(0, std::memory_order_release);  // the slot's previous generation (three back) is over
@@ -467,6 +470,7 @@ struct HipIpcOps {
       sl.first_k.store(k, std::memory_order_release);
       sl.id.store(s->next_id++, std::memory_order_release);
       o.first_k[i] = k;
+      o.epoch = s->epoch;
       o.cur = i;
     }
     *out = o.ev[o.cur];

@@ -153,3 +153,24 @@ def test_rccl_default_policy_at_baseline_size():
     assert par["max_rel"] <= RANK_TOL and par["max_rel_overlapped_exchange"] <= RANK_TOL
     _check_ipc(line)
     assert line["roofline"]["classes"] == 64 and line["config"]["code_bits"] in (20, 24)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_ipc_modes_long_run_shared_device():
+    """The IPC transport past the HIP runtime's 32 records per interprocess event (the 33rd record's
+    wait fails and the event stays broken): tools/ipc_modes_probe.py switches between RCCL, IPC and
+    IPC with per-chunk publication, chunked and not, 26 times with 10 iterations each (~140
+    exchanges per buffer, every event recycled several times); every step must give bitwise the
+    RCCL unchunked ranks on both ranks."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tools", "ipc_modes_probe.py"),
+           "--rounds", "2", "--iters", "10"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    steps = [r for r in recs if "step" in r]
+    assert p.returncode == 0 and steps, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    errors = [r for r in steps if "error" in r]
+    assert not errors, errors[:4]
+    assert len(steps) == 2 * 26 and all(r["bitwise_equal_ref"] for r in steps)
