@@ -540,8 +540,8 @@ def test_hot_reserve_bitwise(hip, oracle_c):
 
 def test_exchange_ipc_option_checks(hip):
     """PR_OPT_XCHG_IPC (the CU-free RCCL-path transport) needs an attached communicator: a single
-    graph refuses it with PR_ERR_STATE and keeps working; values other than 0 / 1 are PR_ERR_INVALID;
-    switching it off when it is off is a no-op."""
+    graph refuses it with PR_ERR_STATE (1, and 2: per-chunk publication) and keeps working; values
+    other than 0 / 1 / 2 are PR_ERR_INVALID; switching it off when it is off is a no-op."""
     from sparky_hip import _lib
 
     rng = np.random.default_rng(5)
@@ -551,7 +551,9 @@ def test_exchange_ipc_option_checks(hip):
         with pytest.raises(Exception, match="communicator"):
             g.set_exchange_ipc(True)
         g.set_exchange_ipc(False)
-        assert _lib.load().pr_set_option(g._h, _lib.PR_OPT_XCHG_IPC, 2) == _lib.PR_ERR_INVALID
+        assert _lib.load().pr_set_option(g._h, _lib.PR_OPT_XCHG_IPC, 2) == _lib.PR_ERR_STATE
+        assert _lib.load().pr_set_option(g._h, _lib.PR_OPT_XCHG_IPC, 3) == _lib.PR_ERR_INVALID
+        assert _lib.load().pr_set_option(g._h, _lib.PR_OPT_XCHG_IPC, -1) == _lib.PR_ERR_INVALID
         r, _ = g.run(3)
         assert np.isfinite(r).all()
 
