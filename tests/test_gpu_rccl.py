@@ -168,7 +168,13 @@ def test_ipc_modes_long_run_shared_device():
            "--rounds", "2", "--iters", "10"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
-    recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    recs, dec = [], json.JSONDecoder()  # two ranks' lines can land on one line of the launcher's stdout
+    for line in p.stdout.splitlines():
+        i = line.find("{")
+        while i >= 0:
+            obj, end = dec.raw_decode(line, i)
+            recs.append(obj)
+            i = line.find("{", end)
     steps = [r for r in recs if "step" in r]
     assert p.returncode == 0 and steps, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
     errors = [r for r in steps if "error" in r]
