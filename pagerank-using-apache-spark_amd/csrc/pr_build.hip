@@ -137,8 +137,7 @@ __global__ void k_order_keys(int32_t V, int b, uint64_t maxd, const int32_t *__r
 }
 
 // rank_of[v] = sorted index; gpos[v] = gather position of v's contribution.  Sorted index i
-// -> part part_of_index(i) (snake order over blocks of P), local rank j = i / P -> class x = j % C,
-// q = j / C -> local row L = x*Q_pad + q.
+// -> part i % P, local rank j = i / P -> class x = j % C, q = j / C -> local row L = x*Q_pad + q.
 __global__ void k_rank_gpos(int32_t V, uint64_t mask, int P, int C, int64_t Q_pad, int64_t S_pad,
                             const uint64_t *__restrict__ sorted_vk, int32_t *__restrict__ rank_of,
                             int32_t *__restrict__ gpos) {
@@ -147,7 +146,7 @@ __global__ void k_rank_gpos(int32_t V, uint64_t mask, int P, int C, int64_t Q_pa
     const int32_t v = (int32_t)(sorted_vk[i] & mask);
     rank_of[v] = (int32_t)i;
     const int64_t j = i / P;
-    gpos[v] = (int32_t)(part_of_index(i, P) * S_pad + (j % C) * Q_pad + j / C);
+    gpos[v] = (int32_t)((i % P) * S_pad + (j % C) * Q_pad + j / C);
   }
 }
 
@@ -157,7 +156,7 @@ struct PartPred {
   int b, P, part;
   __device__ bool operator()(int64_t i) const {
     const int32_t d = (int32_t)(k[i] >> b);
-    return part_of_index(rank_of[d], P) == part;
+    return rank_of[d] % P == part;
   }
 };
 // local key = (segment << (brow + bg)) | (row << bg) | gather position of src, where the
@@ -211,7 +210,7 @@ __global__ void k_local_rows(int64_t R, int64_t n_local, int P, int part, ClassG
       orig[L] = -1;
       continue;
     }
-    const int32_t v = (int32_t)(sorted_vk[index_of_local(j, part, P)] & mask);
+    const int32_t v = (int32_t)(sorted_vk[j * P + part] & mask);
     orig[L] = v;
     uint32_t info = (uint32_t)deg[v];
     if (deg[v] == 0 && (vflags[v] & PR_VF_SINK) && !dangling_none) info |= kRowSink;
@@ -636,7 +635,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
 
   // ---- internal order: out-degree desc, ID asc (hot contributions first) ----
   g->n_local_max = (V + P - 1) / P;
-  g->n_local = part_rows(V, P, part);
+  g->n_local = V > part ? (V - part + P - 1) / P : 0;
   if (max_outdeg > kRowDegMask) return fail(PR_ERR_INVALID, "out-degree above 2^28-1 is not supported");
   // Column classes when the gather space (every part's slice: the columns a part reads) outgrows
   // the L2s (pr_graph.h); their count from the part's expected compacted gather space.

@@ -33,7 +33,7 @@ struct XPred {
   bool send;  // send: u owned here, v elsewhere; receive: v owned here, u elsewhere
   __device__ bool operator()(int64_t i) const {
     const uint64_t key = k[i];
-    const int pu = part_of_index(rank_of[(int32_t)(key & mask)], P), pv = part_of_index(rank_of[(int32_t)(key >> b)], P);
+    const int pu = rank_of[(int32_t)(key & mask)] % P, pv = rank_of[(int32_t)(key >> b)] % P;
     return send ? (pu == part && pv != part) : (pv == part && pu != part);
   }
 };
@@ -49,7 +49,7 @@ struct XKey {
     const uint64_t key = k[i];
     const int32_t u = (int32_t)(key & mask), v = (int32_t)(key >> b);
     const int64_t gu = gpos[u];
-    const int pu = part_of_index(rank_of[u], P), pv = part_of_index(rank_of[v], P);
+    const int pu = rank_of[u] % P, pv = rank_of[v] % P;
     const uint64_t peer = (uint64_t)(send ? pv : pu);
     return (peer << 32) | (uint64_t)(gu - (int64_t)pu * S_pad);
   }

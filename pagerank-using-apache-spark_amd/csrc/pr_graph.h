@@ -2,8 +2,7 @@
 //
 // HBM layout of one part (DESIGN.md "Data layout"):
 //   internal vertex order   vertices sorted by (out-degree desc, original ID asc); sorted index
-//                           i is owned by part part_of_index(i, P) (pr_internal.h: snake order
-//                           over blocks of P) as local rank j = i / P.  Hot sources (high
+//                           i is owned by part i % P as local rank j = i / P.  Hot sources (high
 //                           out-degree = most-gathered contributions) sit together at the front.
 //   slice                   S_pad doubles per part: the contributions c = r/d of its rows, then
 //                           two slots {dangling partial, L1 partial}.

@@ -97,25 +97,6 @@ __host__ __device__ inline int unit_n(const Unit &u) { return u.n & 0xFFFF; }
 __host__ __device__ inline int unit_cls(const Unit &u) { return u.n >> 16; }
 
 // ---- column classes (pr_graph.h "split" layout) -----------------------------------------------
-// Row partition of the internal vertex order (sorted index i, out-degree descending): block
-// b = i / P of P consecutive vertices is dealt to the P parts in snake order (part i % P in even
-// blocks, P - 1 - i % P in odd ones), local rank j = i / P.  Plain round-robin gave part 0 the
-// heaviest vertex of every block, and its pass ran 5-8 % behind the mean at P = 2/4/8
-// (profiles/r05/parts/); the snake alternates who gets it.
-__host__ __device__ inline int part_of_index(int64_t i, int P) {
-  const int64_t b = i / P;
-  const int r = (int)(i - b * P);
-  return (b & 1) ? P - 1 - r : r;
-}
-__host__ __device__ inline int64_t index_of_local(int64_t j, int part, int P) {
-  return j * P + ((j & 1) ? P - 1 - part : part);
-}
-inline int64_t part_rows(int64_t V, int P, int part) {  // local ranks j of `part` with index < V
-  const int64_t nb = V / P, rem = V % P;
-  if (rem == 0) return nb;
-  return nb + (((nb & 1) ? part >= P - rem : part < rem) ? 1 : 0);
-}
-
 constexpr int kXcds = 8;                             // XCDs of the MI355X (one L2 each)
 constexpr int64_t kL2BytesPerXcd = 4ll << 20;        // class count: a class region should fit one L2
 constexpr int kMaxClasses = 128;                     // 8, 16, 32, 64 or 128 (PR_BOPT_CLASSES)

@@ -3,9 +3,7 @@ libpagerank_hip (pr_graph.h layout, pr_iter.hip exchange) in numpy and must repr
 single-process oracle.
 
 What is exercised is the distributed *protocol* the library implements with RCCL on GPUs:
-  * vertex order by (out-degree desc, ID asc); sorted index i -> part part_of(i) (snake order over
-    blocks of P: i % P in even blocks, P - 1 - i % P in odd ones, pr_internal.h part_of_index),
-    local row i / P;
+  * vertex order by (out-degree desc, ID asc); sorted index i -> part i % P, local row i / P;
   * gather space of P slices x S_pad doubles: contributions, then the two slots
     {dangling partial, L1 partial} at S_pad-2 / S_pad-1;
   * one exchange per iteration, every rank summing the P dangling partials in part order (so dc
@@ -22,19 +20,6 @@ import pytest
 
 import sparky_rdd
 
-def part_of(i, P):
-    """pr_internal.h part_of_index: the snake deal of the degree order over the parts"""
-    i = np.asarray(i, np.int64)
-    r = i % P
-    return np.where((i // P) % 2 == 1, P - 1 - r, r)
-
-
-def part_rows(order, P, p):
-    """the original IDs of part p's rows in local order (sorted index i with part_of(i) == p)"""
-    idx = np.arange(order.size)
-    return order[idx[part_of(idx, P) == p]]
-
-
 def layout(csr, P):
     V = csr.n_vertices
     order = np.lexsort((np.arange(V), -csr.out_deg.astype(np.int64)))  # deg desc, id asc
@@ -42,7 +27,7 @@ def layout(csr, P):
     rank_of[order] = np.arange(V)
     n_local_max = (V + P - 1) // P
     S_pad = ((n_local_max + 2 + 63) // 64) * 64
-    gpos = part_of(rank_of, P) * S_pad + rank_of // P
+    gpos = (rank_of % P) * S_pad + rank_of // P
     return order, rank_of, S_pad, gpos
 
 
@@ -50,7 +35,7 @@ def exchange_lists(rank, P, csr, rank_of, S_pad, gpos):
     """Absolute gather positions rank sends to / receives from every peer (pr_exchange.hip
     build_list): sources of cross-part in-links, deduplicated, ascending, then the two slots."""
     V = csr.n_vertices
-    owner = part_of(rank_of, P)
+    owner = rank_of % P
     rows = np.repeat(np.arange(V), np.diff(csr.row_ptr))  # in-link rows (dst)
     cols = csr.col_idx.astype(np.int64)  # sources
     send, recv = {}, {}
@@ -66,7 +51,7 @@ def exchange_lists(rank, P, csr, rank_of, S_pad, gpos):
 
 def part_iteration(rank, P, csr, order, rank_of, S_pad, gpos, iters, exchange):
     V = csr.n_vertices
-    rows = part_rows(order, P, rank)  # original IDs of this part's rows, local order
+    rows = order[rank::P]  # original IDs of this part's rows, local order
     n_local = rows.size
     deg = csr.out_deg[rows]
     sink = (csr.vflags[rows] & 2) != 0
@@ -198,7 +183,7 @@ def test_layout_balances_parts(oracle_c):
     csr = oracle_c.build_csr(len(names), np.array(src, np.int32), np.array(dst, np.int32))
     for P in (2, 4, 8):
         order, rank_of, S_pad, gpos = layout(csr, P)
-        sizes = [part_rows(order, P, p).size for p in range(P)]
+        sizes = [order[p::P].size for p in range(P)]
         assert max(sizes) - min(sizes) <= 1
         assert len(set(gpos.tolist())) == csr.n_vertices  # gather positions are distinct
         assert np.all(gpos % S_pad < S_pad - 2)  # never on a slot
