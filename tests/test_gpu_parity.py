@@ -428,8 +428,7 @@ def test_row_partition_group_on_one_gpu(hip, oracle_c, P, layout, xmode):
             assert sum(i["xchg_send"] for i in infos) == sum(i["xchg_recv"] for i in infos)
         rank_of = np.empty(V, np.int64)
         rank_of[np.lexsort((np.arange(V), -csr.out_deg))] = np.arange(V)
-        r = rank_of % P  # pr_internal.h part_of_index: the degree order dealt in snake order over blocks of P
-        owner = np.where((rank_of // P) % 2 == 1, P - 1 - r, r)
+        owner = rank_of % P
         rows = np.repeat(np.arange(V), np.diff(csr.row_ptr))
         for q, i in enumerate(infos):
             need = np.unique(csr.col_idx[(owner[rows] == q) & (owner[csr.col_idx] != q)])
