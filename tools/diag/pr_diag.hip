@@ -2,6 +2,8 @@
 // code; tools/diag_gather.py, tools/diag_ta.py): random 8-byte gathers by cache policy and memory
 // type, and the address unit's cost per active lane.  Self-contained: no product kernels here (A/B
 // variants of those are separate builds of libpagerank_hip, PR_LIB_PATH).
+#include <chrono>
+#include <vector>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -401,6 +403,40 @@ int prd_scalar_probe(int device, int64_t table_bytes, int64_t n_loads, int per_w
   (void)hipEventDestroy(b);
   (void)hipFree(tab);
   (void)hipFree(out);
+  return 0;
+}
+
+
+// Copy probe: `nstreams` streams each copy `bytes` device to device, all at once, `iters` times;
+// nocu = 1: hipMemcpyDeviceToDeviceNoCU (the copy engines, what the IPC exchange uses), 0: the
+// runtime's default (a blit kernel on the CUs).  Returns ms per round (all streams' copies).
+int prd_copy_probe(int device, int64_t bytes, int nstreams, int nocu, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  if (nstreams < 1 || nstreams > 16) return -1;
+  std::vector<void *> src(nstreams, nullptr), dst(nstreams, nullptr);
+  std::vector<hipStream_t> st(nstreams, nullptr);
+  for (int i = 0; i < nstreams; ++i) {
+    PR_HIP(hipMalloc(&src[i], (size_t)bytes));
+    PR_HIP(hipMalloc(&dst[i], (size_t)bytes));
+    PR_HIP(hipMemset(src[i], 1, (size_t)bytes));
+    PR_HIP(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+  }
+  PR_HIP(hipDeviceSynchronize());
+  const hipMemcpyKind kind = nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
+  double best = 1e30;
+  for (int rep = 0; rep < iters + 1; ++rep) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < nstreams; ++i) PR_HIP(hipMemcpyAsync(dst[i], src[i], (size_t)bytes, kind, st[i]));
+    for (int i = 0; i < nstreams; ++i) PR_HIP(hipStreamSynchronize(st[i]));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rep > 0 && ms < best) best = ms;
+  }
+  *ms_out = best;
+  for (int i = 0; i < nstreams; ++i) {
+    (void)hipStreamDestroy(st[i]);
+    (void)hipFree(src[i]);
+    (void)hipFree(dst[i]);
+  }
   return 0;
 }
 
