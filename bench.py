@@ -257,11 +257,14 @@ def contract_error_line(world: int, steps: int, warmup: int, msg: str) -> dict:
             "roofline": None, "cpu_baseline": None, "error": msg}
 
 
-EXCHANGE_MODES = [("unchunked", False, 0, 0), ("chunked_reserve0", True, 0, 0),
-                  ("chunked_reserve1", True, 1, 0), ("chunked_reserve2", True, 2, 0)]
-# (name, chunked, CU reserve, IPC: 0 = RCCL, 1 = copy-engine pulls, 2 = pulls of each chunk as soon as
-# the peer's epilogue has written it -- per-chunk publication)
-IPC_MODES = [("ipc_unchunked", False, 0, 1), ("ipc_chunked", True, 0, 1), ("ipc_chunked_early", True, 0, 2)]
+EXCHANGE_MODES = [("unchunked", False, 0, 0, 0), ("chunked_reserve0", True, 0, 0, 0),
+                  ("chunked_reserve1", True, 1, 0, 0), ("chunked_reserve2", True, 2, 0, 0)]
+# (name, chunked, CU reserve, IPC: 0 = RCCL, 1 = pulls from the peers' IPC-mapped runs, 2 = pulls of each
+# chunk as soon as the peer's epilogue has written it -- per-chunk publication, VERDICT r4 item 2 --,
+# blit: the pulls run as the runtime's blit kernel (CUs, link speed) instead of on the copy engines
+# (no CU, ~60 GB/s per engine: profiles/r05/copy_engines.log))
+IPC_MODES = [("ipc_unchunked", False, 0, 1, 0), ("ipc_chunked", True, 0, 1, 0), ("ipc_chunked_early", True, 0, 2, 0),
+             ("ipc_blit_unchunked", False, 0, 1, 1), ("ipc_blit_chunked_early", True, 0, 2, 1)]
 
 
 def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chunks: int, device: str = "cuda",
@@ -329,13 +332,14 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
         raise RuntimeError("IPC set-up succeeded on this rank but not on every rank")
     modes = EXCHANGE_MODES + (IPC_MODES if ipc_ok else [])
     best, rejected = None, {}
-    for name, chunked, reserve, ipc in modes:
+    for name, chunked, reserve, ipc, blit in modes:
         if ipc and not ipc_ok:
             continue
         err, same = None, False
         try:
             if ipc_ok:
                 g.set_exchange_ipc(ipc)
+                g.set_exchange_ipc_blit(bool(blit))
             g.set_exchange_chunks(chunked)
             g.set_hot_reserve(reserve)
             same = name == "unchunked" or bool(np.array_equal(local_after(k_chk), ref_local))
@@ -364,12 +368,13 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
         ms = cal_steps(k_cal)
         overlap[f"{name}_ms_per_step"] = ms
         if best is None or ms < best[0]:
-            best = (ms, (name, chunked, reserve, ipc))
+            best = (ms, (name, chunked, reserve, ipc, blit))
     if rejected:
         overlap["rejected"] = rejected
     mode = best[1]
     if ipc_ok:
         g.set_exchange_ipc(mode[3])
+        g.set_exchange_ipc_blit(bool(mode[4]))
     g.set_exchange_chunks(mode[1])
     g.set_hot_reserve(mode[2])
     overlap["chosen"] = mode[0]
@@ -643,6 +648,7 @@ def main() -> int:
         def set_mode(m):
             if ipc_ok:
                 g.set_exchange_ipc(m[3])
+                g.set_exchange_ipc_blit(bool(m[4]))
             g.set_exchange_chunks(m[1])
             g.set_hot_reserve(m[2])
 
@@ -764,7 +770,8 @@ def main() -> int:
                 "n_edges_raw": E,
                 "n_edges_dedup": n_edges,
                 "parallelism": f"row-partition x{world}" + (
-                    (" + copy-engine pulls from IPC-mapped peer send runs" if mode[3] else xchg_desc)
+                    ((" + blit-kernel" if mode[4] else " + copy-engine") + " pulls from IPC-mapped peer send runs"
+                     if mode[3] else xchg_desc)
                     if world > 1 else ""),
                 "exchange_mode": mode[0] if world > 1 else None,
                 "exchange_doubles_per_iter_rank0": info.get("xchg_send", 0) if world > 1 else 0,

@@ -188,6 +188,11 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
  * Collective like PR_OPT_XCHG_CHUNKS (which it combines with); the first enable maps the peers'
  * buffers and fails with PR_ERR_COMM on every rank if any rank cannot. */
 #define PR_OPT_XCHG_IPC 3
+/* PR_OPT_XCHG_IPC_BLIT: how this rank's IPC pulls move the bytes: 0 = the copy engines
+ * (hipMemcpyDeviceToDeviceNoCU, the default: no CU taken from the SpMV, but ~60 GB/s per engine),
+ * 1 = the runtime's blit kernel on the CUs (link speed; it competes with the SpMV for CUs).  Local
+ * to the rank (not collective); no effect on results. */
+#define PR_OPT_XCHG_IPC_BLIT 4
 int pr_set_option(pr_graph *g, int32_t option, int64_t value);
 
 /* Multi-process (one process per GPU): rank 0 creates an id, the host ships the 128 bytes

@@ -294,6 +294,12 @@ int pr_set_option(pr_graph *g, int32_t option, int64_t value) {
     if (g->C > 1) PR_TRY(pr::set_hot_reserve(g, (int)value));
     return PR_OK;
   }
+  if (option == PR_OPT_XCHG_IPC_BLIT) {
+    if (value != 0 && value != 1) return fail(PR_ERR_INVALID, "PR_OPT_XCHG_IPC_BLIT: 0 (copy engines) or 1 (blit kernel)");
+    PR_TRY(pr::join_exchange(g));  // a pending exchange finishes with the old mover
+    g->x_ipc_blit = value == 1;
+    return PR_OK;
+  }
   if (option == PR_OPT_XCHG_IPC) {
     if (value < 0 || value > 2)
       return fail(PR_ERR_INVALID, "PR_OPT_XCHG_IPC: 0 (RCCL), 1 (IPC copy engines) or 2 (IPC, per-chunk publication)");

@@ -172,6 +172,9 @@ struct pr_graph {
   // soon as they are written (per-chunk sent records, pr_ipc_protocol.h), so the peers' pulls of
   // chunk c overlap this rank's epilogue of the later chunks
   bool x_ipc_early = false;
+  // PR_OPT_XCHG_IPC_BLIT: the pulls run as the runtime's blit kernel (CUs, link speed) instead of
+  // on the copy engines (no CU, ~60 GB/s per engine, profiles/r05/copy_engines.log)
+  bool x_ipc_blit = false;
   // recorded on the compute stream when the gather buffer the next exchange fills is no longer read
   // (the start of an iteration / reset): the IPC copy streams wait for it, not for the whole pass
   hipEvent_t x_free_ev = nullptr;

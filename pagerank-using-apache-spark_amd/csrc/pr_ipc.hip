@@ -514,7 +514,8 @@ struct HipIpcOps {
       const double *src = static_cast<const double *>(s->peer_sbuf[q]) + (int64_t)(b & 1) * s->peer_stride[q] +
                           s->peer_soff_me[q] + r0;
       PR_HIP(hipMemcpyAsync(g->cbuf[b].as<double>() + g->S_pad + g->x_roff[q] + r0, src,
-                            sizeof(double) * (size_t)(r1 - r0), hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
+                            sizeof(double) * (size_t)(r1 - r0),
+                            g->x_ipc_blit ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToDeviceNoCU, s->cstream[q]));
     }
     hipEvent_t e = s->cev[(size_t)q * nc + (hi - 1)];
     PR_HIP(hipEventRecord(e, s->cstream[q]));

@@ -47,6 +47,7 @@ PR_CB_RANKS = 1
 PR_OPT_XCHG_CHUNKS = 1
 PR_OPT_HOT_RESERVE = 2
 PR_OPT_XCHG_IPC = 3
+PR_OPT_XCHG_IPC_BLIT = 4
 PR_COMM_ID_BYTES = 128
 
 # Every symbol include/pagerank_hip.h declares (checked by tests/test_abi.py).

@@ -225,6 +225,12 @@ class PageRankGraph:
             raise ValueError("exchange ipc mode must be 0, 1 or 2")
         check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_IPC, v))
 
+    def set_exchange_ipc_blit(self, on: bool) -> None:
+        """pr_set_option(PR_OPT_XCHG_IPC_BLIT): this rank's IPC pulls run as the runtime's blit kernel
+        (True: CUs, link speed) or on the copy engines (False, the default: ~60 GB/s per engine).
+        Local to the rank."""
+        check(_lib.load().pr_set_option(self._h, _lib.PR_OPT_XCHG_IPC_BLIT, 1 if on else 0))
+
     # -- multi-process -------------------------------------------------------------------------
     def attach_comm(self, rank: int, n_ranks: int, uid: bytes) -> None:
         buf = (ctypes.c_uint8 * _lib.PR_COMM_ID_BYTES).from_buffer_copy(uid)

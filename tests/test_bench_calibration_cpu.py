@@ -26,7 +26,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 class FakeGraph:
     def __init__(self, rank, V, script):
         self.rank, self.V, self.script = rank, V, script
-        self.ipc = self.chunked = False
+        self.ipc = self.chunked = self.blit = False
         self.reserve = 0
         self.k = 0
         self.switches = []
@@ -34,7 +34,8 @@ class FakeGraph:
 
     def mode(self):
         if self.ipc:
-            return ("ipc_chunked_early" if self.ipc == 2 else "ipc_chunked") if self.chunked else "ipc_unchunked"
+            b = "blit_" if self.blit else ""
+            return (f"ipc_{b}chunked_early" if self.ipc == 2 else f"ipc_{b}chunked") if self.chunked else f"ipc_{b}unchunked"
         return f"chunked_reserve{self.reserve}" if self.chunked else "unchunked"
 
     def set_exchange_ipc(self, on):
@@ -44,6 +45,9 @@ class FakeGraph:
         if not on and self.script.get("switch_back_fails_on") == self.rank and self.stepped_ipc:
             raise RuntimeError("quiesce failed")
         self.ipc = on
+
+    def set_exchange_ipc_blit(self, on):
+        self.blit = bool(on)
 
     def set_exchange_chunks(self, on):
         self.chunked = on
@@ -120,7 +124,7 @@ def test_all_modes_agree_and_are_candidates():
     ov = r0["overlap"]
     assert r0["ipc_ok"] and "rejected" not in ov and "ipc_error" not in ov
     for name in ("unchunked", "chunked_reserve0", "chunked_reserve1", "chunked_reserve2", "ipc_unchunked",
-                 "ipc_chunked", "ipc_chunked_early"):
+                 "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early"):
         assert ov[f"{name}_ms_per_step"] > 0
     assert ov["candidates_bitwise_checked"] is True
 

@@ -61,7 +61,7 @@ def _check_ipc(line):
     ab, par = line["exchange_overlap_ab"], line["parity"]
     assert "ipc_error" not in ab, ab.get("ipc_error")
     assert ab["candidates_bitwise_checked"] is True and not ab.get("rejected"), ab.get("rejected")
-    names = ("ipc_unchunked", "ipc_chunked", "ipc_chunked_early")
+    names = ("ipc_unchunked", "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early")
     for name in names:  # early: per-chunk publication of the send runs
         assert ab[f"{name}_ms_per_step"] > 0
         assert par[f"{name}_bitwise_equal_rccl"] is True
@@ -103,7 +103,9 @@ def test_rccl_exchange_on_shared_device(world, extra):
         assert line["config"]["exchange_doubles_per_iter_rank0"] > 0
         ab = line["exchange_overlap_ab"]
         assert ab is not None and ab["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1",
-                                                   "chunked_reserve2", "ipc_unchunked", "ipc_chunked")
+                                                   "chunked_reserve2", "ipc_unchunked", "ipc_chunked",
+                                                   "ipc_chunked_early", "ipc_blit_unchunked",
+                                                   "ipc_blit_chunked_early")
         assert par["max_rel_overlapped_exchange"] <= RANK_TOL
         _check_ipc(line)
 
@@ -160,9 +162,9 @@ def test_rccl_default_policy_at_baseline_size():
 def test_ipc_modes_long_run_shared_device():
     """The IPC transport past the HIP runtime's 32 records per interprocess event (the 33rd record's
     wait fails and the event stays broken): tools/ipc_modes_probe.py switches between RCCL, IPC and
-    IPC with per-chunk publication, chunked and not, 26 times with 10 iterations each (~140
-    exchanges per buffer, every event recycled several times); every step must give bitwise the
-    RCCL unchunked ranks on both ranks."""
+    IPC with per-chunk publication, chunked and not, copy engines or blit kernel, 32 times with 10
+    iterations each (~170 exchanges per buffer, every event recycled several times); every step
+    must give bitwise the RCCL unchunked ranks on both ranks."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tools", "ipc_modes_probe.py"),
            "--rounds", "2", "--iters", "10"]
@@ -179,4 +181,4 @@ def test_ipc_modes_long_run_shared_device():
     assert p.returncode == 0 and steps, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
     errors = [r for r in steps if "error" in r]
     assert not errors, errors[:4]
-    assert len(steps) == 2 * 26 and all(r["bitwise_equal_ref"] for r in steps)
+    assert len(steps) == 2 * 32 and all(r["bitwise_equal_ref"] for r in steps)

@@ -16,7 +16,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 
-SEQ = [(0, 0), (1, 0), (1, 1), (2, 1), (2, 0), (0, 1), (1, 1), (2, 1), (1, 0), (2, 1), (0, 0), (2, 1), (2, 1)]
+# (PR_OPT_XCHG_IPC, PR_OPT_XCHG_CHUNKS, PR_OPT_XCHG_IPC_BLIT)
+SEQ = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (2, 1, 0), (2, 0, 0), (0, 1, 0), (1, 1, 1), (2, 1, 0), (1, 0, 1), (2, 1, 1),
+       (0, 0, 0), (2, 1, 0), (2, 1, 1), (1, 1, 0), (1, 0, 0), (2, 1, 0)]
 
 
 def main():
@@ -59,12 +61,13 @@ def main():
         return out
 
     ref = None
-    seq = SEQ * a.rounds if a.only < 0 else [(0, 0)] + [(a.only, 1)] * (len(SEQ) * a.rounds)
+    seq = SEQ * a.rounds if a.only < 0 else [(0, 0, 0)] + [(a.only, 1, 0)] * (len(SEQ) * a.rounds)
     n_err = 0
-    for i, (ipc, chunks) in enumerate(seq):
-        rec = {"rank": rank, "step": i, "ipc": ipc, "chunks": chunks}
+    for i, (ipc, chunks, blit) in enumerate(seq):
+        rec = {"rank": rank, "step": i, "ipc": ipc, "chunks": chunks, "blit": blit}
         try:
             g.set_exchange_ipc(ipc)
+            g.set_exchange_ipc_blit(bool(blit))
             g.set_exchange_chunks(bool(chunks))
             r = run()
             if ref is None:
