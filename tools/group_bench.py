@@ -97,6 +97,9 @@ def main():
         print(json.dumps({"graph": a.graph, "scale": a.scale, "parts": P, "mode": "allgather" if a.allgather else "sparse",
                           "ms_per_iter_all_parts_one_gpu": round(ms, 3), "max_rel_vs_1part": rel,
                           "code_bits": [i["code_bits"] for i in infos], "classes": [i["classes"] for i in infos],
+                          "local_edges": [i["local_edges"] for i in infos], "local_rows": [i["local_rows"] for i in infos],
+                          "hot_cover": [round(i.get("hot_cover_ppm", 0) / 1e6, 4) for i in infos],
+                          "partial_slots": [i.get("partial_slots") for i in infos],
                           "xchg_recv_doubles": recv, "xchg_send_doubles": send,
                           "recv_frac_of_allgather": round(sum(recv) / max(sum(whole), 1), 4)}), flush=True)
         assert rel is None or rel <= 1e-11, rel
