@@ -60,6 +60,38 @@ __global__ __launch_bounds__(256) void k_ta_probe(const double *__restrict__ tab
   }
   if (acc == 12345.0) out[t] = acc;
 }
+// Mixed probe: every thread issues 8 random vector gathers per round (all lanes active) and every
+// wave S random scalar loads (wave-uniform addresses: s_load through the scalar cache) in the same
+// round.  If the time stays that of S = 0 as S grows, the scalar path adds gather capacity beside
+// the vector path (the cold gathers of k_spmv_hot are bound by the vector path's misses in flight).
+template <int S>
+__global__ __launch_bounds__(256) void k_mixed_probe(const double *__restrict__ table, uint32_t n_words, int64_t n_threads,
+                                                     int rounds, uint32_t seed, double *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_threads) return;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, n_words * 8u, 0x00020000);
+  const __attribute__((address_space(4))) double *ct = (const __attribute__((address_space(4))) double *)table;
+  const uint32_t wu = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t >> 6));
+  double acc = 0.0, sacc = 0.0;
+  for (int r = 0; r < rounds; ++r) {
+    double v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t w = mix32((uint32_t)t * 8u + j + seed + (uint32_t)r * 7919u) % n_words;
+      v[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, w * 8u, 0, 0));
+    }
+    if constexpr (S > 0) {
+      double sv[S];
+#pragma unroll
+      for (int k = 0; k < S; ++k) sv[k] = ct[mix32(wu * 4099u + (uint32_t)(r * S + k) + seed) % n_words];
+#pragma unroll
+      for (int k = 0; k < S; ++k) sacc += sv[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  if (acc + sacc == 12345.0) out[t] = acc;
+}
 // Line-sharing probe: random 8-byte loads where several accesses hit the same 128-byte line.
 //   MODE 0: g consecutive lanes of one instruction read g different words of one line
 //   MODE 1: each lane's g consecutive instructions read g different words of one line (the
@@ -437,6 +469,50 @@ int prd_copy_probe(int device, int64_t bytes, int nstreams, int nocu, int iters,
     (void)hipFree(src[i]);
     (void)hipFree(dst[i]);
   }
+  return 0;
+}
+
+// Mixed probe (see k_mixed_probe): n_threads threads x rounds x 8 vector gathers, plus S scalar
+// loads per wave per round; returns ms per launch.
+int prd_mixed_probe(int device, int64_t table_bytes, int64_t n_threads, int rounds, int S, int iters, double *ms_out) {
+  PR_HIP(hipSetDevice(device));
+  void *tab = nullptr, *out = nullptr;
+  PR_HIP(hipMalloc(&tab, (size_t)table_bytes));
+  PR_HIP(hipMemset(tab, 0, (size_t)table_bytes));
+  PR_HIP(hipMalloc(&out, 8 * (size_t)n_threads));
+  const uint32_t nw = (uint32_t)(table_bytes / 8);
+  const dim3 grid((unsigned)((n_threads + 255) / 256));
+  hipEvent_t a, b;
+  PR_HIP(hipEventCreate(&a));
+  PR_HIP(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    PR_HIP(hipEventRecord(a, 0));
+    for (int i = 0; i < (rep ? iters : 1); ++i) {
+      const double *T = (const double *)tab;
+      double *O = (double *)out;
+      switch (S) {
+        case 0: hipLaunchKernelGGL(k_mixed_probe<0>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 1: hipLaunchKernelGGL(k_mixed_probe<1>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 2: hipLaunchKernelGGL(k_mixed_probe<2>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 4: hipLaunchKernelGGL(k_mixed_probe<4>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 8: hipLaunchKernelGGL(k_mixed_probe<8>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 16: hipLaunchKernelGGL(k_mixed_probe<16>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 32: hipLaunchKernelGGL(k_mixed_probe<32>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        case 64: hipLaunchKernelGGL(k_mixed_probe<64>, grid, dim3(256), 0, 0, T, nw, n_threads, rounds, 977u * i, O); break;
+        default: return -1;
+      }
+    }
+    PR_HIP(hipGetLastError());
+    PR_HIP(hipEventRecord(b, 0));
+    PR_HIP(hipEventSynchronize(b));
+  }
+  float ms = 0;
+  PR_HIP(hipEventElapsedTime(&ms, a, b));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipFree(tab);
+  (void)hipFree(out);
   return 0;
 }
 

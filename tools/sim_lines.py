@@ -1,7 +1,7 @@
 """Could k_spmv_hot's cold gathers share cache lines?  (Round 5; CPU simulation, numpy.)
 
 tools/diag_lines.py measured on MI355X that a gather instruction costs the vector-memory path per
-distinct 128-byte line (profiles/r05/diag_lines.log: g lanes of one instruction on one line run g
+distinct 128-byte line (profiles/r05/diag/diag_lines.log: g lanes of one instruction on one line run g
 times faster up to g = 8; one lane's consecutive instructions on one line at most 2.25x).  So if the
 sources a (row, class) segment reads sat side by side in the class region, its cold gathers would
 get cheaper.  This counts, for an R-MAT graph with the bench's parameters, the cold in-links (not in
