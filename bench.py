@@ -271,14 +271,16 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
                        k_chk: int = 3):
     """N > 1: pick the exchange mode of the timed run.  Modes: whole runs after the pass (the
     library default), overlapped with the next SpMV's phases with 0 / 1 / 2 CUs per XCD left to
-    the transfer kernels (which cannot share a CU with k_spmv_hot), and the CU-free IPC transport
-    unchunked / chunked (pr_set_option, collective).  A mode is a candidate only once k_chk of its
-    steps gave, on every rank, bitwise the ranks of the RCCL unchunked exchange (an
-    unverified transport is never timed).  Every outcome -- an exception on any rank, a mismatch --
-    is MIN-reduced over the ranks, so they all decide alike; a failed IPC trial switches every
-    rank back to RCCL together, and a failure of that switch ends the run (RuntimeError -> error
-    line).  The fastest candidate (max over ranks) wins.  Returns (report, mode, ipc_ok); mode =
-    (name, chunked, reserve, ipc), already applied."""
+    the transfer kernels (which cannot share a CU with k_spmv_hot), and the IPC transport (pulls
+    from the peers' mapped send runs: whole, chunked, chunked with per-chunk publication; on the
+    copy engines or as the blit kernel; pr_set_option, collective).  A mode is a candidate only once
+    k_chk of its steps gave, on every rank, bitwise the ranks of the RCCL unchunked exchange (ADVICE
+    r4: an unverified transport is never timed).  Every outcome -- an exception on any rank during
+    the check or the timing, a mismatch -- is MIN-reduced over the ranks between the local work and
+    the next collective, so they all decide alike and no rank waits in a collective alone; a failed
+    IPC trial switches every rank back to RCCL together, and a failure of that switch ends the run
+    (RuntimeError -> error line).  The fastest candidate (max over ranks) wins.  Returns (report,
+    mode, ipc_ok); mode = (name, chunked, reserve, ipc, blit), already applied."""
     import numpy as np
     import torch
 
@@ -291,22 +293,15 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         return bool(t.item())
 
-    def cal_steps(k):
-        g.reset()
-        g.step(warmup)
-        g.sync()
-        dist.barrier()
-        sync()
-        t0 = time.perf_counter()
-        g.step(k)
-        g.sync()
-        sync()
-        tc = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-        dist.barrier()
-        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
-        return round(float(tc.item()) / max(k, 1) * 1e3, 4)
+    def local(fn):
+        """fn() on this rank: (result, error string or None); no collective inside"""
+        try:
+            return fn(), None
+        except Exception as e:  # noqa: BLE001 -- agreed by the caller
+            log(f"exchange mode trial failed on rank {rank}: {e}")
+            return None, str(e)
 
-    def local_after(k):
+    def ranks_after(k):
         """this rank's rows after k iterations from a fresh reset in the current mode"""
         g.reset()
         g.step(k)
@@ -315,11 +310,24 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
         g.ranks(out)
         return out
 
+    def warm():
+        g.reset()
+        g.step(warmup)
+        g.sync()
+        sync()
+
+    def timed(k):
+        t0 = time.perf_counter()
+        g.step(k)
+        g.sync()
+        sync()
+        return time.perf_counter() - t0
+
     overlap = {"calibration_steps": k_cal, "check_steps": k_chk, "chunks": chunks,
                "library_default": "unchunked", "candidates_bitwise_checked": True}
     g.set_exchange_chunks(False)
     g.set_hot_reserve(0)
-    ref_local = local_after(k_chk)  # RCCL, whole runs: the library default
+    ref_local = ranks_after(k_chk)  # RCCL, whole runs: the library default
     ipc_ok = False
     try:  # the IPC set-up is collective and fails on every rank alike (agreed inside the library)
         g.set_exchange_ipc(True)
@@ -331,47 +339,64 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
     if not agree(ipc_ok) and ipc_ok:
         raise RuntimeError("IPC set-up succeeded on this rank but not on every rank")
     modes = EXCHANGE_MODES + (IPC_MODES if ipc_ok else [])
-    best, rejected = None, {}
+    timings, rejected = [], {}
+
+    def failed(name, ipc, err):
+        """every rank saw the failure of mode `name`: an RCCL mode ends the run, an IPC mode drops
+        the IPC modes and switches every rank back to RCCL together"""
+        nonlocal ipc_ok
+        if not ipc:
+            raise RuntimeError(f"exchange mode {name} failed on a rank ({err or 'a peer'})")
+        overlap["ipc_error"] = f"{name}: {err or 'failed on a peer'}"
+        ipc_ok = False
+        back = True
+        try:
+            g.set_exchange_ipc(False)
+            g.set_exchange_ipc_blit(False)
+        except Exception as e2:
+            log(f"switching back to RCCL failed: {e2}")
+            back = False
+        if not agree(back):
+            raise RuntimeError(f"IPC trial failed ({overlap['ipc_error']}) and the switch back to RCCL failed on a rank")
+
     for name, chunked, reserve, ipc, blit in modes:
         if ipc and not ipc_ok:
             continue
-        err, same = None, False
-        try:
+
+        def check():
             if ipc_ok:
                 g.set_exchange_ipc(ipc)
                 g.set_exchange_ipc_blit(bool(blit))
             g.set_exchange_chunks(chunked)
             g.set_hot_reserve(reserve)
-            same = name == "unchunked" or bool(np.array_equal(local_after(k_chk), ref_local))
-        except Exception as e:
-            err = f"{name}: {e}"
-            log(f"exchange mode trial failed on rank {rank}: {e}")
+            return name == "unchunked" or bool(np.array_equal(ranks_after(k_chk), ref_local))
+
+        same, err = local(check)
         if not agree(err is None):
-            if not ipc:
-                raise RuntimeError(f"exchange mode {name} failed on a rank ({err or 'a peer'})")
-            overlap["ipc_error"] = err or f"{name}: failed on a peer"
-            ipc_ok = False
-            back = True
-            try:
-                g.set_exchange_ipc(False)
-            except Exception as e2:
-                log(f"switching back to RCCL failed: {e2}")
-                back = False
-            if not agree(back):
-                raise RuntimeError(f"IPC trial failed ({overlap['ipc_error']}) and the switch back to RCCL "
-                                   "failed on a rank")
+            failed(name, ipc, err)
             continue
-        if not agree(same):  # bitwise on every rank, or not a candidate
+        if not agree(bool(same)):  # bitwise on every rank, or not a candidate
             rejected[name] = f"ranks after {k_chk} steps differ from the RCCL unchunked exchange's"
             log(f"exchange mode {name} rejected: not bitwise equal to RCCL unchunked")
             continue
-        ms = cal_steps(k_cal)
+        _, err = local(warm)
+        if not agree(err is None):
+            failed(name, ipc, err)
+            continue
+        dist.barrier()
+        secs, err = local(lambda: timed(k_cal))
+        if not agree(err is None):
+            failed(name, ipc, err)
+            continue
+        tc = torch.tensor([secs], dtype=torch.float64, device=device)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        ms = round(float(tc.item()) / max(k_cal, 1) * 1e3, 4)
         overlap[f"{name}_ms_per_step"] = ms
-        if best is None or ms < best[0]:
-            best = (ms, (name, chunked, reserve, ipc, blit))
+        timings.append((ms, (name, chunked, reserve, ipc, blit)))
     if rejected:
         overlap["rejected"] = rejected
-    mode = best[1]
+    # the fastest mode still allowed (an IPC failure after some IPC modes were timed drops them all)
+    mode = min((t for t in timings if ipc_ok or not t[1][3]), key=lambda t: t[0])[1]
     if ipc_ok:
         g.set_exchange_ipc(mode[3])
         g.set_exchange_ipc_blit(bool(mode[4]))

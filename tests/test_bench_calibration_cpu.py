@@ -62,6 +62,8 @@ class FakeGraph:
         self.stepped_ipc = self.stepped_ipc or self.ipc
         if self.script.get("raise_in") == (self.rank, self.mode()):
             raise RuntimeError("PR_ERR_COMM: peer never enqueued its sent record")
+        if self.script.get("raise_in_timing") == (self.rank, self.mode()) and k == 2:  # k_cal = 2 below
+            raise RuntimeError("IPC exchange: wait failed (invalid argument)")
         self.k += k
 
     def sync(self):
@@ -182,3 +184,19 @@ def test_parity_failures_null_the_value():
         assert bench.parity_failures(bad), k
     bad = dict(good, modes={"ipc_chunked": {"max_rel": 1e-15, "bitwise_equal_rccl_unchunked": False}})
     assert bench.parity_failures(bad)
+
+
+def test_failure_during_the_timing_on_one_rank_is_agreed():
+    """A mode that passes its bitwise check but fails while it is being timed (round 5: an event past
+    the runtime's record limit) on ONE rank: no rank waits in a collective alone, every rank drops
+    the IPC modes and switches back, and the chosen mode is an RCCL one on every rank."""
+    res = _run({"raise_in_timing": (1, "ipc_chunked")})
+    _same_decision(res)
+    for v in res.values():
+        ov = v["overlap"]
+        assert v["ipc_ok"] is False and v["final_ipc"] is False
+        assert "ipc_chunked" in ov["ipc_error"] and "ipc_chunked_ms_per_step" not in ov
+        assert "ipc_unchunked_ms_per_step" in ov  # timed before the failure
+        # IPC was dropped after ipc_unchunked had been timed: the choice falls back to an RCCL mode
+        assert ov["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1", "chunked_reserve2")
+        assert v["mode"][3] == 0
