@@ -406,6 +406,84 @@ def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chun
     return overlap, mode, ipc_ok
 
 
+def parity_runs(g, dist, rank: int, V: int, K: int, mode, ipc_ok: bool, all_modes: bool, device: str = "cuda"):
+    """The GPU side of the parity leg: K iterations from a fresh reset in the RCCL unchunked
+    exchange (the reference every other mode must equal bit for bit on every rank), then -- with
+    all_modes -- in the timed configuration itself (its chunking, hot reserve and transport) and in
+    every other transport setting the calibration could pick, each on its own.  A failure on any
+    rank is agreed before the reductions (no rank waits in one alone); a mode that fails is recorded
+    and every rank switches back to the reference together.  Returns (the reference ranks summed
+    over the ranks on rank 0, every row owned exactly once, {mode: (merged ranks on rank 0, bitwise
+    equal to the reference on every rank)}, {mode: error})."""
+    import numpy as np
+    import torch
+
+    def agree_all(ok: bool) -> bool:
+        if dist is None:
+            return ok
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
+
+    def gpu_ranks():
+        """(this rank's rows, every rank's rows summed on rank 0, every row owned exactly once)"""
+        mine = np.zeros(V, np.float64)
+        err = None
+        try:
+            g.reset()
+            g.step(K)
+            g.sync()
+            g.ranks(mine)  # this rank's rows; the others stay 0
+        except Exception as e:  # noqa: BLE001 -- agreed below
+            err = e
+        if not agree_all(err is None):
+            raise RuntimeError(f"parity run failed on a rank: {err or 'a peer failed'}")
+        merged, owned_once = mine, True
+        if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
+            rt = torch.from_numpy(mine).to(device)
+            own = torch.from_numpy((mine != 0).astype(np.int32)).to(device)
+            dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
+            dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                merged = rt.cpu().numpy()
+                owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
+            del rt, own
+        return mine, merged, owned_once
+
+    def set_mode(m):
+        if ipc_ok:
+            g.set_exchange_ipc(m[3])
+            g.set_exchange_ipc_blit(bool(m[4]))
+        g.set_exchange_chunks(m[1])
+        g.set_hot_reserve(m[2])
+
+    ref_mode = EXCHANGE_MODES[0]
+    set_mode(ref_mode)
+    ref_local, ref_merged, owned_once = gpu_ranks()
+    checked, failed = {}, {}
+    if all_modes:
+        others = [mode] + [m for m in [EXCHANGE_MODES[1]] + IPC_MODES if m[0] != mode[0] and (ipc_ok or not m[3])]
+        for m in others:
+            if m[0] == ref_mode[0]:
+                continue
+            try:
+                set_mode(m)
+                loc, merged, oc = gpu_ranks()
+            except Exception as e:  # noqa: BLE001 -- a mode that cannot run fails the parity check
+                failed[m[0]] = str(e)
+                log(f"parity run of mode {m[0]} failed: {e}")
+                try:
+                    set_mode(ref_mode)
+                except Exception as e2:  # noqa: BLE001
+                    raise RuntimeError(f"mode {m[0]} failed ({e}) and the switch back to RCCL failed ({e2})")
+                continue
+            owned_once = owned_once and oc
+            checked[m[0]] = (merged if rank == 0 else None, agree_all(bool(np.array_equal(loc, ref_local))))
+            del loc
+        set_mode(ref_mode)
+    return ref_merged, owned_once, checked, failed
+
+
 def launch_ranks(a) -> int:
     """`python bench.py --gpus N` (N > 1) outside a launcher: start N ranks under
     torch.distributed.run as a CHILD process (this parent never imports torch or touches a GPU, and
@@ -636,85 +714,7 @@ def main() -> int:
     if validate:
         K = a.parity_iters
 
-        def agree_all(ok: bool) -> bool:
-            if dist is None:
-                return ok
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            return bool(t.item())
-
-        def gpu_ranks():
-            """K iterations from a fresh reset in the current mode: (this rank's rows, every rank's rows
-            summed on rank 0, every row owned exactly once).  A failure on any rank is agreed before the
-            reductions (so no rank waits in one alone) and raised on every rank."""
-            mine = np.zeros(V, np.float64)
-            err = None
-            try:
-                g.reset()
-                g.step(K)
-                g.sync()
-                g.ranks(mine)  # this rank's rows; the others stay 0
-            except Exception as e:  # noqa: BLE001 -- agreed below
-                err = e
-            if not agree_all(err is None):
-                raise RuntimeError(f"parity run failed on a rank: {err or 'a peer failed'}")
-            merged, owned_once = mine, True
-            if dist is not None:  # each vertex is owned by exactly one rank: the sum is exact
-                rt = torch.from_numpy(mine).cuda()
-                own = torch.from_numpy((mine != 0).astype(np.int32)).cuda()
-                dist.reduce(rt, dst=0, op=dist.ReduceOp.SUM)
-                dist.reduce(own, dst=0, op=dist.ReduceOp.SUM)
-                if rank == 0:
-                    merged = rt.cpu().numpy()
-                    owned_once = int(own.min().item()) == 1 and int(own.max().item()) == 1
-                del rt, own
-            return mine, merged, owned_once
-
-        def set_mode(m):
-            if ipc_ok:
-                g.set_exchange_ipc(m[3])
-                g.set_exchange_ipc_blit(bool(m[4]))
-            g.set_exchange_chunks(m[1])
-            g.set_hot_reserve(m[2])
-
-        def all_ranks_equal(x, y) -> bool:
-            ok = bool(np.array_equal(x, y))
-            if dist is None:
-                return ok
-            t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            return bool(t.item())
-
-        # the RCCL unchunked exchange (the library default) is the reference every other mode must
-        # equal bit for bit on every rank; then the timed configuration itself (its chunking, hot
-        # reserve and transport), and every other transport setting the calibration could pick
-        ref_mode = EXCHANGE_MODES[0]
-        set_mode(ref_mode)
-        ref_local, mine, owned_once = gpu_ranks()
-        checked = {}  # name -> (merged ranks on rank 0, bitwise equal to the reference on every rank)
-        failed = {}
-        if overlap is not None:
-            others = [mode] + [m for m in [EXCHANGE_MODES[1]] + IPC_MODES if m[0] != mode[0] and (ipc_ok or not m[3])]
-            failed = {}
-            for m in others:
-                if m[0] == ref_mode[0]:
-                    continue
-                try:
-                    set_mode(m)
-                    loc, merged, oc = gpu_ranks()
-                except Exception as e:  # noqa: BLE001 -- a mode that cannot run fails the parity check
-                    failed[m[0]] = str(e)
-                    log(f"parity run of mode {m[0]} failed: {e}")
-                    try:
-                        set_mode(ref_mode)
-                    except Exception as e2:  # noqa: BLE001
-                        raise RuntimeError(f"mode {m[0]} failed ({e}) and the switch back to RCCL failed ({e2})")
-                    continue
-                owned_once = owned_once and oc
-                checked[m[0]] = (merged if rank == 0 else None, all_ranks_equal(loc, ref_local))
-                del loc
-            set_mode(ref_mode)
-        del ref_local
+        mine, owned_once, checked, failed = parity_runs(g, dist, rank, V, K, mode, ipc_ok, overlap is not None)
         if rank == 0:
             try:
                 res, threads, desc, e_csr, same = oracle_leg(g, V, K, pick_threads=True, raw=raw or None)

@@ -96,7 +96,28 @@ def _worker(rank, world, port, q, script):
         dist.destroy_process_group()
 
 
-def _run(script, world=2):
+def _parity_worker(rank, world, port, q, script):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+
+        g = FakeGraph(rank, 16, script)
+        timed = next(m for m in bench.IPC_MODES if m[0] == script.get("timed", "ipc_unchunked"))
+        try:
+            merged, owned, checked, failed = bench.parity_runs(g, dist, rank, 16, 4, timed, True, True, device="cpu")
+            q.put((rank, {"checked": {k: v[1] for k, v in checked.items()}, "failed": sorted(failed),
+                          "final_ipc": g.ipc}))
+        except RuntimeError as e:
+            q.put((rank, {"error": str(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(script, world=2, worker=None):
     import torch.multiprocessing as mp
 
     with socket.socket() as s:
@@ -104,7 +125,7 @@ def _run(script, world=2):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, script)) for r in range(world)]
+    procs = [ctx.Process(target=worker or _worker, args=(r, world, port, q, script)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
@@ -200,3 +221,18 @@ def test_failure_during_the_timing_on_one_rank_is_agreed():
         # IPC was dropped after ipc_unchunked had been timed: the choice falls back to an RCCL mode
         assert ov["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1", "chunked_reserve2")
         assert v["mode"][3] == 0
+
+
+def test_parity_leg_records_a_failing_mode_on_every_rank():
+    """bench.parity_runs (the GPU side of the parity leg): a mode that raises on ONE rank is recorded
+    as failed on every rank (its failure is agreed before the rank reductions), a mode whose ranks
+    differ on ONE rank is not bitwise equal on every rank, the others are checked, and every rank
+    ends on the RCCL reference."""
+    res = _run({"raise_in": (1, "ipc_chunked"), "differs_in": (0, "ipc_blit_unchunked"), "timed": "ipc_unchunked"},
+               worker=_parity_worker)
+    for v in res.values():
+        assert "error" not in v, v
+        assert v["failed"] == ["ipc_chunked"]
+        assert v["checked"]["ipc_unchunked"] is True and v["checked"]["chunked_reserve0"] is True
+        assert v["checked"]["ipc_blit_unchunked"] is False
+        assert v["final_ipc"] == 0
