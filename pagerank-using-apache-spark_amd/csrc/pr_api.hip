@@ -2,6 +2,7 @@
 // the run loop with its per-iteration callback, export, and the RCCL exchange.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <new>
@@ -9,6 +10,7 @@
 #include <vector>
 
 #include "pr_graph.h"
+#include "pr_xcheck.h"
 
 namespace pr {
 
@@ -417,7 +419,10 @@ int pr_graph_attach_comm(pr_graph *g, int32_t rank, int32_t n_ranks, const uint8
     return fail(PR_ERR_INVALID, "rank/n_ranks must equal the graph's part/n_parts");
   if (g->comm) return fail(PR_ERR_STATE, "communicator already attached");
   DeviceGuard dg(g->device);
-  if (!g->comm_scratch.p) PR_TRY(g->comm_scratch.alloc(pr::kCommScratchBytes));
+  if (!g->comm_scratch.p) {  // the IPC set-up's records and the exchange agreement records
+    const size_t xrec = sizeof(int64_t) * (size_t)pr::xrec_width(n_ranks) * (size_t)(n_ranks + 1);
+    PR_TRY(g->comm_scratch.alloc(std::max(pr::kCommScratchBytes, xrec)));
+  }
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof(uid));
   ncclResult_t rc = ncclCommInitRank(&g->comm, n_ranks, uid, rank);

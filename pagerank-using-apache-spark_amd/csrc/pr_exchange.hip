@@ -334,13 +334,16 @@ int verify_exchange(pr_graph *g) {
   std::vector<int64_t> mine(W, 0);
   if (!xrec_fill(g->V, g->S_pad, g->x_allgather, nc, g->x_chunked, P, g->x_soff.data(), g->x_sch.data(), mine.data()))
     return fail(PR_ERR_INVALID, "too many exchange chunks");
-  DevBuf d;
-  PR_TRY(d.alloc(sizeof(int64_t) * (size_t)W * (P + 1)));
-  PR_HIP(hipMemcpyAsync(d.as<int64_t>(), mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, g->stream));
-  ncclResult_t rc = ncclAllGather(d.as<int64_t>(), d.as<int64_t>() + W, (size_t)W, ncclInt64, g->comm, g->stream);
+  // through the scratch allocated with the communicator (sized for this record), so no rank can fail
+  // an allocation here and leave its peers waiting in the all-gather
+  if (g->comm_scratch.bytes < sizeof(int64_t) * (size_t)W * (P + 1))
+    return fail(PR_ERR_STATE, "communicator scratch too small for the exchange records");
+  int64_t *d = static_cast<int64_t *>(g->comm_scratch.p);
+  PR_HIP(hipMemcpyAsync(d, mine.data(), sizeof(int64_t) * W, hipMemcpyHostToDevice, g->stream));
+  ncclResult_t rc = ncclAllGather(d, d + W, (size_t)W, ncclInt64, g->comm, g->stream);
   if (rc != ncclSuccess) return fail(PR_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(rc));
   std::vector<int64_t> all((size_t)W * P);
-  PR_HIP(hipMemcpyAsync(all.data(), d.as<int64_t>() + W, sizeof(int64_t) * W * P, hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipMemcpyAsync(all.data(), d + W, sizeof(int64_t) * W * P, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
   const char *why = "";
   const int rv = xrec_check(all.data(), P, g->part, mine.data(), g->x_roff.data(), g->x_rch.data(), nc, &why);
