@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--mode", type=int, default=2, help="PR_OPT_XCHG_IPC: 1 or 2")
     ap.add_argument("--chunks", type=int, default=1, help="PR_OPT_XCHG_CHUNKS")
+    ap.add_argument("--blit", type=int, default=0, help="PR_OPT_XCHG_IPC_BLIT: pulls as the blit kernel")
     ap.add_argument("--iters", type=int, default=6)
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -62,6 +63,7 @@ def main():
     info = g.info()
     g.set_exchange_chunks(bool(a.chunks))
     g.set_exchange_ipc(a.mode)
+    g.set_exchange_ipc_blit(bool(a.blit))
     out = {}
     for mode in (a.mode,):
         g.reset()
@@ -74,7 +76,7 @@ def main():
         out[f"mode{mode}_ms_per_iter"] = (time.perf_counter() - t0) / a.iters * 1e3
     r = np.zeros(V)
     g.ranks(r)
-    out.update(rank=rank, world=world, mode=a.mode, chunks=a.chunks, classes=info["classes"],
+    out.update(rank=rank, world=world, mode=a.mode, chunks=a.chunks, blit=a.blit, classes=info["classes"],
                xchg_recv=info.get("xchg_recv"), checksum=float(r.sum()))
     print(json.dumps(out), flush=True)
     dist.barrier()
