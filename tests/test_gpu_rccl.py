@@ -111,6 +111,20 @@ def test_rccl_exchange_on_shared_device(world, extra):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_rccl_and_ipc_eight_ranks_shared_device():
+    """The driver's largest rank count: 8 ranks (7 peers per rank) on the one GPU, R-MAT s20 with 32
+    classes (4 chunks per run) -- every exchange mode calibrated and checked bitwise against the RCCL
+    unchunked exchange, the timed mode and every IPC mode against the oracle."""
+    line = _run(8, ["--build-option", "classes=32"], timeout=380)
+    assert line["n_gpus"] == 8 and line["config"]["shared_device_rehearsal"] is True
+    par = line["parity"]
+    assert par["ranks_from"] == "8 rank(s)" and par["every_row_owned_once"] is True
+    assert par["max_rel"] <= RANK_TOL and par["max_rel_overlapped_exchange"] <= RANK_TOL
+    _check_ipc(line)
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(320)
 def test_ipc_on_distinct_gpus():
     """The IPC transport across physical devices: hipIpcOpenMemHandle with lazy peer
