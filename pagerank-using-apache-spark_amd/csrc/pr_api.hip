@@ -124,6 +124,10 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
         if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_XCHG_SDMA: 0 (device copies) or 1 (copy engines)");
         o->xchg_sdma = v == 1;
         break;
+      case PR_BOPT_EPI_ORDER:
+        if (v != 0 && v != 1) return fail(PR_ERR_INVALID, "PR_BOPT_EPI_ORDER: 0 (row order) or 1 (heaviest first)");
+        o->epi_order = v == 1;
+        break;
       default:
         return fail(PR_ERR_INVALID, "unknown build option " + std::to_string(k));
     }

@@ -961,6 +961,7 @@ int build_graph(pr_graph *g, int64_t E, const int32_t *src_in, const int32_t *ds
     const bool auto_narrow = g->n_walk_groups * 10 >= ngrp;
     g->epi_narrow = epi_narrow_ok(C) && (g->opts.epi_narrow < 0 ? auto_narrow : g->opts.epi_narrow != 0);
     g->ep_blocks = (int)grid_for(ngrp, epi_grp_threads(g->epi_narrow) / kWave, 1u << 20);
+    PR_TRY(plan_epi_order(g));
   }
   // the split epilogue writes one {dangling, L1} partial per group (pr_spmv.h epi_group)
   const int64_t ep_parts = C > 1 ? (g->nblk + kEpiGroup - 1) / kEpiGroup : 0;

@@ -47,6 +47,7 @@ struct pr_build_opts {
   int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
   bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
   bool xchg_sdma = false;  // group path: runs move on the copy engines (hipMemcpyDeviceToDeviceNoCU)
+  bool epi_order = true;   // epilogue groups dispatched heaviest first (PR_BOPT_EPI_ORDER)
 };
 
 struct pr_graph {
@@ -102,6 +103,10 @@ struct pr_graph {
   bool epi_narrow = false;  // one-wave epilogue workgroups (PR_BOPT_EPI_NARROW; default: many walking groups)
   int64_t n_walk_groups = 0;
   pr::DevBuf eoff, epos;
+  // dispatch order of the epilogue groups (PR_BOPT_EPI_ORDER): epi_ord[k] = the group the k-th
+  // wave takes, heaviest first; [0, ngrp) for the whole pass, [ngrp, 2 ngrp) sorted within each
+  // exchange chunk's group range (the per-chunk epilogue of PR_OPT_XCHG_IPC = 2)
+  pr::DevBuf epi_ord;
   int64_t n_hunits = 0, n_segs = 0, nblk = 0, n_slots = 0;
   int64_t hot_cover_ppm = 0;  // in-links whose source is in a class's hot set (layout policy input)
   pr::DevBuf cbuf[2];
@@ -198,6 +203,7 @@ constexpr size_t kCommScratchBytes = 256 << 10;
 int build_graph(pr_graph *g, int64_t n_edges, const int32_t *src, const int32_t *dst);
 int iter_reset(pr_graph *g, const double *init_ranks_host);
 int plan_epi_walk(pr_graph *g);  // per-row walk of sparse epilogue groups (after rmask/cbase)
+int plan_epi_order(pr_graph *g);  // dispatch order of the epilogue groups (after cbase)
 int prepare_hot_kernel();  // lets k_spmv_hot use up to 160 KiB of dynamic LDS (current device)
 // the heavy-row pass (k_spmv_hot) on g's stream, hot phases [ph0, ph1) (-1: all)
 int launch_hot(pr_graph *g, int in_buf, int ph0 = 0, int ph1 = -1);

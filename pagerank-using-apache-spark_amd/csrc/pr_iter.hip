@@ -23,7 +23,9 @@
 //   P > 1: the exchange (pr_exchange.hip) sends every peer the contributions its in-links read.
 //
 // Every sum has a fixed order, so results are bitwise reproducible run to run.
+#include <algorithm>
 #include <climits>
+#include <vector>
 
 #include "pr_device.h"
 #include "pr_graph.h"
@@ -232,6 +234,61 @@ int plan_epi_walk(pr_graph *g) {
   return PR_OK;
 }
 
+namespace {
+// partial slots of every epilogue group: its class runs [cbase[b0][x], cbase[b0 + nb][x]) summed
+__global__ __launch_bounds__(kThreads) void k_epi_cost(int64_t nblk, int C, const int32_t *__restrict__ cbase,
+                                                       int32_t *__restrict__ cost) {
+  const int64_t ngrp = (nblk + kEpiGroup - 1) / kEpiGroup;
+  const int64_t gi = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (gi >= ngrp) return;
+  const int64_t b0 = gi * kEpiGroup, b1 = min(nblk, b0 + kEpiGroup);
+  int64_t n = 0;
+  for (int x = 0; x < C; ++x) n += (int64_t)cbase[b1 * C + x] - cbase[b0 * C + x];
+  cost[gi] = (int32_t)min(n, (int64_t)INT32_MAX);
+}
+}  // namespace
+
+// Dispatch order of the epilogue groups (PR_BOPT_EPI_ORDER).  A group's wave stages its class runs
+// batch after batch, so a group holding the first (highest in-degree) rows of a class region runs
+// for tens of microseconds while most groups take a few; in row order those groups sit at the
+// start of every class region and the last regions' ones are dispatched last, into the tail of the
+// kernel -- most visible for the parts of a row partition (8 K groups at s26 P = 8 against 64 K
+// at P = 1).  The workgroups are dispatched in blockIdx order, so the order below (slots
+// descending, row order among equals) starts the heaviest groups first.  The per-chunk launches of
+// PR_OPT_XCHG_IPC = 2 take positions [lo, hi) of chunk ranges: their order is sorted within each.
+int plan_epi_order(pr_graph *g) {
+  g->epi_ord.reset();
+  if (!g->opts.epi_order || g->C <= 1 || g->nblk <= 0) return PR_OK;
+  const int64_t ngrp = (g->nblk + kEpiGroup - 1) / kEpiGroup;
+  DevBuf dcost;
+  PR_TRY(dcost.alloc(sizeof(int32_t) * (size_t)ngrp));
+  hipLaunchKernelGGL(k_epi_cost, dim3((unsigned)((ngrp + kThreads - 1) / kThreads)), dim3(kThreads), 0, g->stream,
+                     g->nblk, g->C, g->cbase.as<int32_t>(), dcost.as<int32_t>());
+  PR_HIP(hipGetLastError());
+  std::vector<int32_t> cost((size_t)ngrp), ord(2 * (size_t)ngrp);
+  PR_HIP(hipMemcpyAsync(cost.data(), dcost.p, sizeof(int32_t) * (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  auto heavier = [&](int32_t a, int32_t b) { return cost[a] != cost[b] ? cost[a] > cost[b] : a < b; };
+  auto sort_range = [&](int32_t *o, int64_t lo, int64_t hi) {
+    for (int64_t k = lo; k < hi; ++k) o[k] = (int32_t)k;
+    std::sort(o + lo, o + hi, heavier);
+  };
+  sort_range(ord.data(), 0, ngrp);
+  const int nxc = std::max(1, g->C / kXcds);  // the exchange chunks (pr_exchange.hip n_xc)
+  const int64_t rows_per_grp = (int64_t)kEpiGroup * kWave, chunk_rows = (int64_t)kXcds * g->Q_pad;
+  int64_t lo = 0;
+  for (int c = 0; c < nxc; ++c) {
+    const int64_t hi = std::max(lo, ipc_epi_chunk_end(ngrp, c, nxc, chunk_rows, rows_per_grp));
+    sort_range(ord.data() + ngrp, lo, hi);
+    lo = hi;
+  }
+  if (lo < ngrp) sort_range(ord.data() + ngrp, lo, ngrp);
+  PR_TRY(g->epi_ord.alloc(sizeof(int32_t) * ord.size()));
+  PR_HIP(hipMemcpyAsync(g->epi_ord.p, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice, g->stream));
+  PR_HIP(hipStreamSynchronize(g->stream));
+  return PR_OK;
+}
+
 int n_hot_phases(const pr_graph *g) { return g->C > 1 ? std::max(1, g->C / kXcds) : 1; }
 
 int set_hot_reserve(pr_graph *g, int per_xcd) {
@@ -379,17 +436,19 @@ int iter_compute(pr_graph *g) {
       pd.self = g->part;
       for (int q = 0; q < g->nparts; ++q) pd.soff[q] = g->x_soff[q];
     }
+    const int64_t ngrp = epi_groups(g);
+    // dispatch order (plan_epi_order): the whole pass, or sorted within each chunk's range
+    const int32_t *ord = g->epi_ord.p ? g->epi_ord.as<int32_t>() + (ipc_early(g) ? ngrp : 0) : nullptr;
     auto epilogue = [&](int64_t g_lo, int64_t g_hi, unsigned grid) -> int {
       hipLaunchKernelGGL(epi, dim3(grid), dim3(epi_grp_threads(g->epi_narrow)), epi_grp_lds(g->epi_narrow), s,
                          g->nblk, g_lo, g_hi, g->partial.as<double>(), g->rmask.p, g->cbase.as<int32_t>(),
                          g->rowinfo.as<uint32_t>(), g->r.as<double>(), g->cbuf[out].as<double>() + own,
                          g->cbuf[in].as<double>(), g->slots, (double)g->V, g->teleport, g->damping,
                          g->unit_part.as<double2>() + g->n_units, g->eoff.as<int64_t>(), g->epos.as<uint16_t>(),
-                         g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(), pd);
+                         g->x_pmask.as<uint8_t>(), g->x_sbase.as<int32_t>(), ord, pd);
       PR_HIP(hipGetLastError());
       return PR_OK;
     };
-    const int64_t ngrp = epi_groups(g);
     if (!ipc_early(g)) {
       PR_TRY(epilogue(0, ngrp, (unsigned)g->ep_blocks));
     } else {

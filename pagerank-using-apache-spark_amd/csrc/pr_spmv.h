@@ -1039,7 +1039,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
 }
 
 //
-// Groups [g_lo, g_hi) of the pass (all of them in the product).
+// Dispatch positions [g_lo, g_hi) of the pass (all of them in the product).
 #ifndef PR_EPI_WAVES
 #define PR_EPI_WAVES 0  // > 0: amdgpu_waves_per_eu floor of k_epilogue_grp (A/B builds)
 #endif
@@ -1055,7 +1055,7 @@ __global__ PR_EPI_BOUNDS(NT) void k_epilogue_grp(
     double *__restrict__ cout, const double *__restrict__ cin, SlotPos sp, double n_vertices, double teleport,
     double damping, double2 *__restrict__ ep_part /* [group] */, const int64_t *__restrict__ eoff,
     const uint16_t *__restrict__ epos, const uint8_t *__restrict__ pmask, const int32_t *__restrict__ sbase,
-    PackDst pd) {
+    const int32_t *__restrict__ order, PackDst pd) {
   constexpr int W = kEpiWin;
   constexpr int NW = NT / kWave;
   extern __shared__ double epi_lds[];  // NW windows of W + 2 slots
@@ -1066,7 +1066,10 @@ __global__ PR_EPI_BOUNDS(NT) void k_epilogue_grp(
   if (lane == 0) win[W] = 0.0;  // the zero slot (never a DMA target: fill <= W)
   const double tdc = dc_from_slots(cin, sp) / n_vertices;
   const int64_t nw = (int64_t)gridDim.x * NW;
-  for (int64_t gi = g_lo + (int64_t)blockIdx.x * NW + wv; gi < g_hi; gi += nw) epi_group<C, WALK>(a, pd, gi, tdc, win, ep_part);
+  // order: the group of each dispatch position (heaviest first, plan_epi_order); the group's
+  // partials go to its own ep_part slot, so the order changes no sum
+  for (int64_t k = g_lo + (int64_t)blockIdx.x * NW + wv; k < g_hi; k += nw)
+    epi_group<C, WALK>(a, pd, order ? (int64_t)order[k] : k, tdc, win, ep_part);
 }
 
 // Build-time plan of the per-row walk (WALK above), one wave per group of G 64-row blocks.
@@ -1146,7 +1149,7 @@ __global__ __launch_bounds__(kEpiThreads) void k_epi_walk_plan(int64_t nblk, con
 // four-wave workgroups
 using EpiGrpFn = void (*)(int64_t, int64_t, int64_t, const double *, const void *, const int32_t *, const uint32_t *, double *,
                           double *, const double *, SlotPos, double, double, double, double2 *, const int64_t *,
-                          const uint16_t *, const uint8_t *, const int32_t *, PackDst);
+                          const uint16_t *, const uint8_t *, const int32_t *, const int32_t *, PackDst);
 template <int C>
 inline EpiGrpFn epi_grp_kernel_c(bool walk, bool narrow) {
   if constexpr (C <= kWave) {

@@ -40,7 +40,8 @@ INFO_NAMES = ["n_vertices", "n_edges", "n_sink", "n_nolink", "n_indeg0", "max_in
               "walk_groups", "layout", "hot_cover_ppm", "code_bits"]
 # build options of pr_graph_create_ex (PR_BOPT_*), by the keyword PageRankGraph(options=...) takes
 BUILD_OPTIONS = {"classes": 1, "hot_slots": 2, "exchange_allgather": 3, "xchg_chunks": 4, "hot_reserve": 5,
-                 "epi_walk": 6, "epi_narrow": 7, "codes": 8, "pack_fused": 9, "xchg_sdma": 10}
+                 "epi_walk": 6, "epi_narrow": 7, "codes": 8, "pack_fused": 9, "xchg_sdma": 10,
+                 "epi_order": 11}
 STAT_NAMES = ["iters", "last_dc", "last_l1", "spmv_ms_mean", "spmv_launches", "iter_ms_mean",
               "build_ms", "exchange_ms_mean"]
 PR_CB_RANKS = 1

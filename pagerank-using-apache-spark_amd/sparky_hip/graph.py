@@ -70,7 +70,7 @@ class PageRankGraph:
         contribution slice outgrows the L2s), 'fused' or 'split' (pr_graph.h).  options: build
         options of pr_graph_create_ex by name -- _lib.BUILD_OPTIONS is the full list: classes,
         hot_slots, exchange_allgather, xchg_chunks, hot_reserve, epi_walk, epi_narrow, codes,
-        pack_fused, xchg_sdma (include/pagerank_hip.h PR_BOPT_*)."""
+        pack_fused, xchg_sdma, epi_order (include/pagerank_hip.h PR_BOPT_*)."""
         L = _lib.load()
         flags = 0
         if dangling == "none":

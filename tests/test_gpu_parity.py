@@ -740,8 +740,9 @@ def test_compact_codes_widen_then_fall_back(hip, oracle_c, V, bits):
 def test_epilogue_grid_shapes_bitwise(hip, oracle_c, classes):
     """The grouped epilogue writes one {dangling, L1} partial per group of 8 x 64 rows (pr_spmv.h
     epi_group), which k_finalize adds in group order, so the workgroup shape of the epilogue -- one-wave
-    or four-wave workgroups (PR_BOPT_EPI_NARROW), hence a different grid -- does not change a bit of
-    the ranks, dc or L1 of any iteration (Sparky.java:219-222, :229-233)."""
+    or four-wave workgroups (PR_BOPT_EPI_NARROW), hence a different grid -- and the order the groups
+    are dispatched in (heaviest first or row order, PR_BOPT_EPI_ORDER) do not change a bit of the
+    ranks, dc or L1 of any iteration (Sparky.java:219-222, :229-233)."""
     rng = np.random.default_rng(classes)
     V = 60000
     src, dst = random_edges(rng, V, 900000, hub_frac=0.02)
@@ -749,15 +750,17 @@ def test_epilogue_grid_shapes_bitwise(hip, oracle_c, classes):
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), iters, keep_history=True)
     out = {}
     for narrow in (0, 1):
-        with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split",
-                               options={"classes": classes, "epi_narrow": narrow}) as g:
-            assert g.info()["classes"] == classes
-            hist = []
-            ranks, st = g.run(iters, want_ranks_in_callback=True, callback=lambda it, r, s: hist.append((r, s)))
-            out[narrow] = (ranks, hist)
-    (r0, h0), (r1, h1) = out[0], out[1]
-    assert np.array_equal(r0, r1)
-    for it, ((a, sa), (b, sb)) in enumerate(zip(h0, h1)):
-        assert np.array_equal(a, b)
-        assert sa.dangling_sum == sb.dangling_sum and sa.l1_delta == sb.l1_delta
-        assert max_rel(a, ref["history"][it]) <= RANK_TOL
+        for order in (1, 0):
+            with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split",
+                                   options={"classes": classes, "epi_narrow": narrow, "epi_order": order}) as g:
+                assert g.info()["classes"] == classes
+                hist = []
+                ranks, st = g.run(iters, want_ranks_in_callback=True, callback=lambda it, r, s: hist.append((r, s)))
+                out[narrow, order] = (ranks, hist)
+    r0, h0 = out[0, 1]
+    for key, (r1, h1) in out.items():
+        assert np.array_equal(r0, r1), key
+        for it, ((a, sa), (b, sb)) in enumerate(zip(h0, h1)):
+            assert np.array_equal(a, b), key
+            assert sa.dangling_sum == sb.dangling_sum and sa.l1_delta == sb.l1_delta, key
+            assert max_rel(a, ref["history"][it]) <= RANK_TOL
