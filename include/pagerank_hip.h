@@ -139,9 +139,10 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_XCHG_SDMA 10  /* group path (pr_group_*, P > 1 per-peer runs): 0 (default) the runs move by
                                  device copies (ROCclr blit kernels on the CUs), 1 by the copy engines
                                  (hipMemcpyDeviceToDeviceNoCU), which leave k_spmv_hot every CU */
-#define PR_BOPT_EPI_ORDER 11  /* split layout: 1 (default) the epilogue dispatches its groups heaviest first
-                                 (most partial slots; within each exchange chunk when the epilogue runs
-                                 chunk by chunk), 0 in row order; same sums either way */
+#define PR_BOPT_EPI_ORDER 11  /* split layout: the epilogue's dispatch order, 0 (default) row order, 1 runs
+                                 of 8 consecutive groups heaviest first (most partial slots; within each
+                                 exchange chunk when the epilogue runs chunk by chunk), 2 single groups
+                                 heaviest first; same sums either way */
 int pr_graph_create_ex(int32_t device, int32_t part, int32_t n_parts, int32_t n_vertices, int64_t n_edges,
                        const int32_t *src, const int32_t *dst, uint32_t flags, const int64_t *options,
                        int32_t n_options, pr_graph **out);

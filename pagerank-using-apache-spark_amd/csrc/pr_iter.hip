@@ -248,17 +248,19 @@ __global__ __launch_bounds__(kThreads) void k_epi_cost(int64_t nblk, int C, cons
 }
 }  // namespace
 
-// Dispatch order of the epilogue groups (PR_BOPT_EPI_ORDER).  A group's wave stages its class runs
-// batch after batch, so a group holding the first (highest in-degree) rows of a class region runs
-// for tens of microseconds while most groups take a few; in row order those groups sit at the
-// start of every class region and the last regions' ones are dispatched last, into the tail of the
-// kernel -- most visible for the parts of a row partition (8 K groups at s26 P = 8 against 64 K
-// at P = 1).  The workgroups are dispatched in blockIdx order, so the order below (slots
-// descending, row order among equals) starts the heaviest groups first.  The per-chunk launches of
-// PR_OPT_XCHG_IPC = 2 take positions [lo, hi) of chunk ranges: their order is sorted within each.
+// Dispatch order of the epilogue groups (PR_BOPT_EPI_ORDER, off by default).  A group's wave
+// stages its class runs batch after batch, so a group holding the first (highest in-degree) rows
+// of a class region runs far longer than most; in row order those groups sit at the start of
+// every class region and the last regions' ones are dispatched (blockIdx order) last.  Options 1
+// and 2 sort the dispatch by slots, heaviest first: runs of kEpiOrderRun consecutive groups (1) or
+// single groups (2).  Measured: an s26 P = 8 part's epilogue -8 %, the one-GPU
+// pass +2.5 % (every light group then runs at the end), so row order is the default.  The
+// per-chunk launches of PR_OPT_XCHG_IPC = 2 take positions [lo, hi) of chunk ranges: their order
+// is sorted within each.
+constexpr int64_t kEpiOrderRun = 8;
 int plan_epi_order(pr_graph *g) {
   g->epi_ord.reset();
-  if (!g->opts.epi_order || g->C <= 1 || g->nblk <= 0) return PR_OK;
+  if (g->opts.epi_order == 0 || g->C <= 1 || g->nblk <= 0) return PR_OK;
   const int64_t ngrp = (g->nblk + kEpiGroup - 1) / kEpiGroup;
   DevBuf dcost;
   PR_TRY(dcost.alloc(sizeof(int32_t) * (size_t)ngrp));
@@ -268,10 +270,19 @@ int plan_epi_order(pr_graph *g) {
   std::vector<int32_t> cost((size_t)ngrp), ord(2 * (size_t)ngrp);
   PR_HIP(hipMemcpyAsync(cost.data(), dcost.p, sizeof(int32_t) * (size_t)ngrp, hipMemcpyDeviceToHost, g->stream));
   PR_HIP(hipStreamSynchronize(g->stream));
-  auto heavier = [&](int32_t a, int32_t b) { return cost[a] != cost[b] ? cost[a] > cost[b] : a < b; };
+  const int64_t run = g->opts.epi_order == 1 ? kEpiOrderRun : 1;
+  // [lo, hi) in runs of `run` groups from lo, runs by their slots descending, groups in a run in order
   auto sort_range = [&](int32_t *o, int64_t lo, int64_t hi) {
-    for (int64_t k = lo; k < hi; ++k) o[k] = (int32_t)k;
-    std::sort(o + lo, o + hi, heavier);
+    std::vector<std::pair<int64_t, int64_t>> runs;  // (-slots, first group)
+    for (int64_t a = lo; a < hi; a += run) {
+      int64_t n = 0;
+      for (int64_t k = a; k < std::min(hi, a + run); ++k) n += cost[k];
+      runs.emplace_back(-n, a);
+    }
+    std::sort(runs.begin(), runs.end());
+    int64_t w = lo;
+    for (const auto &r : runs)
+      for (int64_t k = r.second; k < std::min(hi, r.second + run); ++k) o[w++] = (int32_t)k;
   };
   sort_range(ord.data(), 0, ngrp);
   const int nxc = std::max(1, g->C / kXcds);  // the exchange chunks (pr_exchange.hip n_xc)

@@ -94,7 +94,7 @@ def test_build_options_match_header_and_are_checked():
     src, dst = np.array([0], np.int32), np.array([1], np.int32)
     for bad in ({"classes": 12}, {"hot_slots": 20000}, {"exchange_allgather": 2}, {"hot_reserve": 4},
                 {"epi_narrow": 2}, {"codes": 1}, {"pack_fused": 2}, {"xchg_sdma": 2}, {"xchg_chunks": 2},
-                {"xchg_chunks": -1}, {"epi_walk": 7}, {"epi_order": 2}):
+                {"xchg_chunks": -1}, {"epi_walk": 7}, {"epi_order": 3}):
         with pytest.raises(sparky_hip.PageRankError) as ei:
             sparky_hip.PageRankGraph(2, src, dst, options=bad)
         assert ei.value.code == L.PR_ERR_INVALID, bad

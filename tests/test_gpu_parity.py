@@ -750,7 +750,7 @@ def test_epilogue_grid_shapes_bitwise(hip, oracle_c, classes):
     ref = oracle_c.run(oracle_c.build_csr(V, src, dst), iters, keep_history=True)
     out = {}
     for narrow in (0, 1):
-        for order in (1, 0):
+        for order in (1, 2, 0):
             with hip.PageRankGraph(V, src, dst, keep_canonical=False, layout="split",
                                    options={"classes": classes, "epi_narrow": narrow, "epi_order": order}) as g:
                 assert g.info()["classes"] == classes
