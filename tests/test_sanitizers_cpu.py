@@ -35,3 +35,32 @@ def test_ipc_model_under_sanitizer(tmp_path, san):
     assert r.returncode == 0 and "done, 0 failures" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
     assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr
     assert "runtime error" not in r.stderr
+
+
+HOST_SRC = [os.path.join(ROOT, "tests", "sanitize", "host_parse_main.cpp"),
+            os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host", "pr_host.cpp")]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("san,threads", [("address,undefined", 1), ("address,undefined", 4), ("thread", 4)])
+def test_host_parsers_fuzzed_under_sanitizer(tmp_path, san, threads):
+    """The host front-ends (the edge list and the Common Crawl JSON records of
+    Sparky.java:61-123) on seeded mutations of valid inputs -- flipped, inserted, NUL and high bytes,
+    truncations, spliced spans: every input parses (and every name and edge is in range) or fails
+    with a message, with no sanitizer report; the reader's worker threads under TSan."""
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    exe = tmp_path / "parse"
+    cmd = [cxx, "-std=c++17", "-O1", "-g", f"-fsanitize={san}", "-fno-sanitize-recover=all", "-pthread",
+           "-I" + os.path.join(ROOT, "pagerank-using-apache-spark_amd", "host"), *INC, *HOST_SRC, "-o", str(exe)]
+    b = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-3000:]
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([str(exe), "3000", str(threads)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and " bad 0" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+    parsed, rejected = (int(x) for x in r.stdout.split()[1:4:2])
+    assert parsed > 0 and rejected > 0  # the corpus reaches both outcomes
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr
+    assert "runtime error" not in r.stderr
