@@ -132,6 +132,10 @@ struct pr_graph {
   std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;
   int64_t spmv_passes = 0;
   size_t ev_next = 0;
+  // ev_pool index of an event recorded on `stream` with nothing enqueued after it yet, which the
+  // next interval may start from instead of recording its own (-1: none); every record is a
+  // marker packet of ~5 us between kernels (R-MAT s20: 4 per iteration were 28 % of it)
+  int ev_start_hint = -1;
 
   // gather space (doubles per cbuf): P slices side by side (P = 1, PR_BOPT_EXCHANGE = 1), or
   // compacted: this part's slice, then the runs received from every peer in peer order

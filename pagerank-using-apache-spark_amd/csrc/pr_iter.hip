@@ -387,8 +387,16 @@ int iter_compute(pr_graph *g) {
   // stream's wait for the exchange, so a transfer still in flight is never counted as SpMV time;
   // the overlapped exchange contributes one interval per hot phase.
   int open_ev = -1;  // ev_pool index of the running interval's start
+  const int hint = g->ev_start_hint;
+  g->ev_start_hint = -1;
+  bool enqueued = false;  // anything on the stream since the hint's record
   auto mark_start = [&]() -> int {
     if (!g->timing) return PR_OK;
+    if (hint >= 0 && !enqueued) {  // the iteration's start event is the pass's start too
+      open_ev = hint;
+      enqueued = true;  // once
+      return PR_OK;
+    }
     hipEvent_t e = next_event(g);
     if (!e) return fail(PR_ERR_HIP, "hipEventCreate failed");
     PR_HIP(hipEventRecord(e, s));
@@ -409,6 +417,8 @@ int iter_compute(pr_graph *g) {
   PR_TRY(ipc_send_runs_free(g, out));  // the epilogue and k_finalize write the runs of `out`
   const int nph = g->C > 1 ? n_hot_phases(g) : 1;
   const bool phased_wait = g->C > 1 && g->n_hunits > 0 && g->x_pending && g->x_chunked && g->n_xc == nph && nph > 1;
+  // one part: nothing above enqueued anything (no exchange, no IPC buffers)
+  enqueued = g->nparts > 1 || g->x_free_ev != nullptr || g->x_pending;
   if (!phased_wait) PR_TRY(join_exchange(g));
   else PR_HIP(hipStreamWaitEvent(s, g->x_ev[0], 0));  // phase 0's chunk
   PR_TRY(mark_start());
@@ -492,14 +502,17 @@ int iter_compute(pr_graph *g) {
 int iter_step(pr_graph *g, int32_t iterations) {
   if (!g->ready) return fail(PR_ERR_STATE, "pr_step before pr_reset");
   if (g->grouped) return fail(PR_ERR_STATE, "graph belongs to a group: use pr_group_step");
+  int carry = -1;  // the previous iteration's end event: nothing was enqueued after it
   for (int32_t it = 0; it < iterations; ++it) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g->timing) {
+    int i0 = carry;
+    if (g->timing && i0 < 0) {
       e0 = next_event(g);
       if (!e0) return fail(PR_ERR_HIP, "hipEventCreate failed");
       PR_HIP(hipEventRecord(e0, g->stream));
+      i0 = (int)g->ev_next - 1;
     }
-    const int i0 = (int)g->ev_next - 1;
+    g->ev_start_hint = g->timing ? i0 : -1;
     PR_TRY(iter_compute(g));
     hipEvent_t xa = nullptr, xb = nullptr;
     if (g->timing && g->nparts > 1) {
@@ -516,6 +529,7 @@ int iter_step(pr_graph *g, int32_t iterations) {
       PR_HIP(hipEventRecord(e1, g->stream));  // compute stream: the iteration's kernels + the pack
       const int i1 = (int)g->ev_next - 1;
       g->iter_ev.push_back({i0, i1});
+      carry = i1;  // the next iteration starts where this one ended (same stream, nothing between)
     }
   }
   return PR_OK;
