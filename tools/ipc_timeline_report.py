@@ -25,7 +25,6 @@ def main():
     epi, cps, hot = {}, {}, {}
     for r in ranks:
         kt = glob.glob(os.path.join(a.dir, f"r{r}", "**", "*kernel_trace.csv"), recursive=True)
-        blit = []  # pulls run as the runtime's blit kernel appear as kernels, not memory copies
         mt = glob.glob(os.path.join(a.dir, f"r{r}", "**", "*memory_copy_trace.csv"), recursive=True)
         ks = rows(kt[0])
         epi[r] = sorted((int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in ks
@@ -35,6 +34,7 @@ def main():
         ms = rows(mt[0]) if mt else []
         d2d = [x for x in ms if "DEVICE_TO_DEVICE" in (x.get("Direction", "") + x.get("Kind", "")).upper()
                or x.get("Source_Agent_Id") == x.get("Destination_Agent_Id")]
+        # pulls run as the runtime's blit kernel (PR_OPT_XCHG_IPC_BLIT) appear as kernels, not copies
         blit = [(int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in ks if "copyBuffer" in x["Kernel_Name"]]
         cps[r] = sorted([(int(x["Start_Timestamp"]), int(x["End_Timestamp"])) for x in d2d] + (blit if not d2d else []))
     t0 = min(v[0][0] for v in epi.values() if v)
