@@ -263,8 +263,11 @@ EXCHANGE_MODES = [("unchunked", False, 0, 0, 0), ("chunked_reserve0", True, 0, 0
 # chunk as soon as the peer's epilogue has written it -- per-chunk publication, VERDICT r4 item 2 --,
 # blit: the pulls run as the runtime's blit kernel (CUs, link speed) instead of on the copy engines
 # (no CU, ~60 GB/s per engine: profiles/r05/copy_engines.log))
+# The blit pulls of the per-chunk publication also run with 1 / 2 CUs per XCD left free by k_spmv_hot
+# (VERDICT r5 item 2): the link-rate mover then has CUs during the hot phases it overlaps.
 IPC_MODES = [("ipc_unchunked", False, 0, 1, 0), ("ipc_chunked", True, 0, 1, 0), ("ipc_chunked_early", True, 0, 2, 0),
-             ("ipc_blit_unchunked", False, 0, 1, 1), ("ipc_blit_chunked_early", True, 0, 2, 1)]
+             ("ipc_blit_unchunked", False, 0, 1, 1), ("ipc_blit_chunked_early", True, 0, 2, 1),
+             ("ipc_blit_chunked_early_reserve1", True, 1, 2, 1), ("ipc_blit_chunked_early_reserve2", True, 2, 2, 1)]
 
 
 def calibrate_exchange(g, dist, V: int, rank: int, k_cal: int, warmup: int, chunks: int, device: str = "cuda",
@@ -457,6 +460,23 @@ def parity_runs(g, dist, rank: int, V: int, K: int, mode, ipc_ok: bool, all_mode
         g.set_exchange_chunks(m[1])
         g.set_hot_reserve(m[2])
 
+    def local(fn):
+        """fn() on this rank: None or its error string; no collective of bench's own inside"""
+        try:
+            fn()
+            return None
+        except Exception as e:  # noqa: BLE001 -- agreed by the caller
+            return str(e)
+
+    def back_to_ref(name, err):
+        """every rank saw mode `name` fail: all switch back to the reference together"""
+        failed[name] = err
+        log(f"parity run of mode {name} failed: {err}")
+        err2 = local(lambda: set_mode(ref_mode))
+        if not agree_all(err2 is None):
+            raise RuntimeError(f"mode {name} failed ({err}) and the switch back to RCCL failed "
+                               f"({err2 or 'on a peer'})")
+
     ref_mode = EXCHANGE_MODES[0]
     set_mode(ref_mode)
     ref_local, ref_merged, owned_once = gpu_ranks()
@@ -466,16 +486,16 @@ def parity_runs(g, dist, rank: int, V: int, K: int, mode, ipc_ok: bool, all_mode
         for m in others:
             if m[0] == ref_mode[0]:
                 continue
+            # a local failure of the switch is agreed before any rank runs the mode (a
+            # rank that failed here must not meet its peers' gpu_ranks reductions with its own)
+            err = local(lambda: set_mode(m))
+            if not agree_all(err is None):
+                back_to_ref(m[0], err or "switching to the mode failed on a peer")
+                continue
             try:
-                set_mode(m)
-                loc, merged, oc = gpu_ranks()
+                loc, merged, oc = gpu_ranks()  # a failure inside is agreed: it raises on every rank
             except Exception as e:  # noqa: BLE001 -- a mode that cannot run fails the parity check
-                failed[m[0]] = str(e)
-                log(f"parity run of mode {m[0]} failed: {e}")
-                try:
-                    set_mode(ref_mode)
-                except Exception as e2:  # noqa: BLE001
-                    raise RuntimeError(f"mode {m[0]} failed ({e}) and the switch back to RCCL failed ({e2})")
+                back_to_ref(m[0], str(e))
                 continue
             owned_once = owned_once and oc
             checked[m[0]] = (merged if rank == 0 else None, agree_all(bool(np.array_equal(loc, ref_local))))

@@ -139,7 +139,8 @@ int pr_graph_create_part(int32_t device, int32_t part, int32_t n_parts, int32_t 
 #define PR_BOPT_XCHG_SDMA 10  /* group path (pr_group_*, P > 1 per-peer runs): 0 (default) the runs move by
                                  device copies (ROCclr blit kernels on the CUs), 1 by the copy engines
                                  (hipMemcpyDeviceToDeviceNoCU), which leave k_spmv_hot every CU */
-#define PR_BOPT_EPI_ORDER 11  /* split layout: the epilogue's dispatch order, 0 (default) row order, 1 runs
+#define PR_BOPT_EPI_ORDER 11  /* split layout: the epilogue's dispatch order, -1 (default) auto: 2 for a
+                                 part of a row partition (n_parts > 1), 0 for one part; 0 row order, 1 runs
                                  of 8 consecutive groups heaviest first (most partial slots; within each
                                  exchange chunk when the epilogue runs chunk by chunk), 2 single groups
                                  heaviest first; same sums either way */
@@ -189,8 +190,9 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats);
  * 2 = as 1, and the epilogue runs chunk by chunk, publishing each chunk's runs as soon as they are
  * written, so (with PR_OPT_XCHG_CHUNKS) a peer's pull of chunk c overlaps this rank's epilogue of
  * the later chunks (the split layout's fused pack with several chunks; otherwise as 1).
- * Collective like PR_OPT_XCHG_CHUNKS (which it combines with); the first enable maps the peers'
- * buffers and fails with PR_ERR_COMM on every rank if any rank cannot. */
+ * Collective like PR_OPT_XCHG_CHUNKS (which it combines with): every rank must pass the same value
+ * (ranks that disagree all fail with PR_ERR_STATE, nothing changed); the first enable maps the
+ * peers' buffers and fails with PR_ERR_COMM on every rank if any rank cannot. */
 #define PR_OPT_XCHG_IPC 3
 /* PR_OPT_XCHG_IPC_BLIT: how this rank's IPC pulls move the bytes: 0 = the copy engines
  * (hipMemcpyDeviceToDeviceNoCU, the default: no CU taken from the SpMV, but ~60 GB/s per engine),

@@ -125,8 +125,9 @@ int parse_options(const int64_t *options, int32_t n, pr_build_opts *o) {
         o->xchg_sdma = v == 1;
         break;
       case PR_BOPT_EPI_ORDER:
-        if (v < 0 || v > 2)
-          return fail(PR_ERR_INVALID, "PR_BOPT_EPI_ORDER: 0 (row order), 1 (runs of 8 groups heaviest first), 2 (groups heaviest first)");
+        if (v < -1 || v > 2)
+          return fail(PR_ERR_INVALID, "PR_BOPT_EPI_ORDER: -1 (auto), 0 (row order), 1 (runs of 8 groups heaviest first), "
+                                      "2 (groups heaviest first)");
         o->epi_order = (int)v;
         break;
       default:

@@ -47,7 +47,7 @@ struct pr_build_opts {
   int codes = -1;        // -1: compact codes where they fit (P = 1), 0: 32-bit codes
   bool pack_fused = true;  // P > 1: the epilogue writes the send runs (no pack kernel)
   bool xchg_sdma = false;  // group path: runs move on the copy engines (hipMemcpyDeviceToDeviceNoCU)
-  int epi_order = 0;       // epilogue dispatch order (PR_BOPT_EPI_ORDER): 0 rows, 1 runs of 8 groups, 2 groups
+  int epi_order = -1;      // epilogue dispatch order (PR_BOPT_EPI_ORDER): -1 auto, 0 rows, 1 runs of 8 groups, 2 groups
 };
 
 struct pr_graph {

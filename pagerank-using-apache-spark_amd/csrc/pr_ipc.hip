@@ -56,6 +56,7 @@
 
 #include "pagerank_hip.h"
 #include "pr_graph.h"
+#include "pr_ipc_gens.h"
 #include "pr_ipc_protocol.h"
 
 namespace pr {
@@ -68,8 +69,16 @@ namespace {
 constexpr double kSpinLimit = 120.0;  // seconds a host waits for a peer's record before failing
 constexpr int kIpcMaxChunks = 16;     // sent events per buffer: one per exchange chunk (C / 8 <= 16)
 
-constexpr int64_t kRecordsPerEvent = 30;  // below the runtime's 32-record ring (see "events" above)
-constexpr int kGens = 3;                  // handle slots per event in the page
+constexpr int64_t kRecordsPerEvent = kIpcRecordsPerEvent;  // pr_ipc_gens.h (see "events" above)
+constexpr int kGens = kIpcGens;                            // handle slots per event in the page
+// A host may run at most 2 * kLeadEvery exchanges ahead of its own device (bound_lead).  An event
+// generation is destroyed (own) or closed (opened) only when an exchange at least
+// (kGens - 1) * kRecordsPerEvent past its last record or wait is enqueued, and the hosts stay within
+// one exchange of each other; so with this bound every record and wait on it has executed on every
+// device by then (without it, one long pr_step let a host destroy an event its device
+// had not reached).
+constexpr int64_t kLeadEvery = 8;
+static_assert(2 * kLeadEvery + 2 < (kGens - 1) * kRecordsPerEvent, "the lead bound must stay below an event's reuse");
 
 // one generation of one event: the exchanges [first_k, first_k + kRecordsPerEvent) it serves
 struct IpcSlot {
@@ -113,9 +122,7 @@ struct IpcState {
   // current slot per (kind, b, c) (-1: none yet); the next generation id
   struct Own {
     hipEvent_t ev[kGens] = {nullptr, nullptr, nullptr};
-    int64_t first_k[kGens] = {0, 0, 0};
-    int64_t epoch = -1;  // of the current generation
-    int cur = -1;
+    IpcGenOwner gen;  // pr_ipc_gens.h
   };
   std::vector<Own> own;  // [(kind * 2 + b) * nc + c]
   int64_t next_id = 1;
@@ -132,6 +139,12 @@ struct IpcState {
   std::vector<hipEvent_t> cev;  // [q * nc + c]
   int nc = 0;
   IpcProtocol<HipIpcOps> proto;  // the host-side ordering (pr_ipc_protocol.h)
+  // the host's lead over its own device, bounded (bound_lead): a local event recorded on the compute
+  // stream every kLeadEvery exchanges, alternating between two; the host waits for an event's
+  // previous record before recording it again
+  hipEvent_t lead_ev[2] = {nullptr, nullptr};
+  bool lead_rec[2] = {false, false};
+  int64_t n_exch = 0;
 };
 
 namespace {
@@ -176,6 +189,8 @@ void free_state(IpcState *s) {
   for (auto &o : s->own)
     for (hipEvent_t e : o.ev)
       if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s->lead_ev)
+    if (e) (void)hipEventDestroy(e);
   for (IpcCounters *c : s->peer) unmap_page(c);
   if (s->mine) {
     unmap_page(s->mine);
@@ -361,15 +376,24 @@ int ipc_setup(pr_graph *g) {
 
 int set_exchange_ipc(pr_graph *g, int mode) {
   const bool on = mode != 0;
-  if (on == g->x_ipc) {
-    g->x_ipc_early = mode == 2;  // per-chunk publication: no effect on the ordering state
-    return PR_OK;
-  }
+  if (!on && !g->x_ipc) return PR_OK;  // off and staying off
   if (on) {
     if (!g->comm || g->comm_size <= 1) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs an attached communicator (P > 1)");
     if (g->x_allgather) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC needs the per-peer runs (PR_BOPT_EXCHANGE = 0)");
   }
   PR_TRY(quiesce(g));
+  // every rank asks for the same mode: a receiver waits for per-chunk records only if
+  // its peers make them (mode 2), so a 1 <-> 2 switch on some ranks only would bind a wait to a
+  // stale generation or fail later; min over the ranks of mode and of -mode must agree
+  int32_t lo = mode, nhi = -mode;
+  PR_TRY(comm_barrier(g, &lo));
+  PR_TRY(comm_barrier(g, &nhi));
+  if (lo != -nhi) return fail(PR_ERR_STATE, "PR_OPT_XCHG_IPC: the ranks asked for different modes (" + std::to_string(lo) +
+                                                " .. " + std::to_string(-nhi) + "); nothing changed");
+  if (on == g->x_ipc) {
+    g->x_ipc_early = mode == 2;  // per-chunk publication: every rank idle, every rank switches
+    return PR_OK;
+  }
   if (on && !g->ipc) PR_TRY(ipc_setup(g));
   // every rank idle (so no copy out of another's buffers is pending) before the mode changes
   int32_t one = 1;
@@ -404,17 +428,14 @@ struct HipIpcOps {
   // range holds k (written before k was published), opened here once per generation
   int peer_event(int q, int kind, int b, int c, int64_t k, hipEvent_t *out) {
     IpcState::Opened &o = s->opened[(((size_t)q * 2 + kind) * 2 + b) * s->nc + c];
-    int best = -1;
-    int64_t best_id = 0;
+    int64_t ids[kGens], firsts[kGens];
     for (int i = 0; i < kGens; ++i) {
       const IpcSlot &sl = s->peer[q]->slot[kind][b][c][i];
-      const int64_t id = sl.id.load(std::memory_order_acquire);
-      const int64_t f = sl.first_k.load(std::memory_order_acquire);
-      if (id > best_id && f <= k && k < f + kRecordsPerEvent) {
-        best = i;
-        best_id = id;
-      }
+      ids[i] = sl.id.load(std::memory_order_acquire);
+      firsts[i] = sl.first_k.load(std::memory_order_acquire);
     }
+    const int best = ipc_gen_pick(ids, firsts, k);
+    const int64_t best_id = best >= 0 ? ids[best] : 0;
     if (best < 0)
       return pr::fail(PR_ERR_COMM, "IPC exchange: peer " + std::to_string(q) + " published exchange " + std::to_string(k) +
                                        " without an event for it");
@@ -457,8 +478,8 @@ struct HipIpcOps {
   // to the page slot before k is published
   int own_event(int kind, int b, int c, int64_t k, hipEvent_t *out) {
     IpcState::Own &o = s->own[((size_t)kind * 2 + b) * s->nc + c];
-    if (o.cur < 0 || o.epoch != s->epoch || k < o.first_k[o.cur] || k >= o.first_k[o.cur] + kRecordsPerEvent) {
-      const int i = (o.cur + 1) % kGens;
+    const int i = ipc_gen_rotate(o.gen, k, s->epoch);
+    if (i >= 0) {
       IpcSlot &sl = s->mine->slot[kind][b][c][i];
       sl.id.store(0, std::memory_order_release);  // the slot's previous generation (three back) is over
       if (o.ev[i]) (void)hipEventDestroy(o.ev[i]);
@@ -469,11 +490,9 @@ struct HipIpcOps {
       std::memcpy(&sl.h, &h, sizeof(h));
       sl.first_k.store(k, std::memory_order_release);
       sl.id.store(s->next_id++, std::memory_order_release);
-      o.first_k[i] = k;
-      o.epoch = s->epoch;
-      o.cur = i;
+      ipc_gen_started(o.gen, i, k, s->epoch);
     }
-    *out = o.ev[o.cur];
+    *out = o.ev[o.gen.cur];
     return PR_OK;
   }
   int record(int kind, int b, int c, int64_t k) {
@@ -555,6 +574,30 @@ int ipc_chunk_sent(pr_graph *g, int buf, int c) {
   return g->ipc->proto.chunk_sent(o, buf, c);
 }
 
+// Every kLeadEvery exchanges: wait (bounded) until the device has passed the compute-stream marker
+// recorded 2 * kLeadEvery exchanges ago, then record it again.  The compute stream waits for the
+// transfers each pass reads, so its progress bounds the copy streams' too.
+static int bound_lead(pr_graph *g, IpcState *s) {
+  if (++s->n_exch % kLeadEvery != 0) return PR_OK;
+  const int j = (int)((s->n_exch / kLeadEvery) & 1);
+  if (!s->lead_ev[j]) PR_HIP(hipEventCreateWithFlags(&s->lead_ev[j], hipEventDisableTiming));
+  if (s->lead_rec[j]) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(s->lead_ev[j]);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) PR_HIP(e);
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > kSpinLimit)
+        return fail(PR_ERR_COMM, "IPC exchange: the device did not reach an exchange enqueued " +
+                                     std::to_string(2 * kLeadEvery) + " exchanges ago (a peer stalled?)");
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  PR_HIP(hipEventRecord(s->lead_ev[j], g->stream));
+  s->lead_rec[j] = true;
+  return PR_OK;
+}
+
 int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   HipIpcOps o{g, g->ipc, ev_a};
   const bool packed = g->x_packed == buf;
@@ -562,7 +605,7 @@ int exchange_ipc(pr_graph *g, int buf, hipEvent_t ev_a, hipEvent_t ev_b) {
   PR_TRY(g->ipc->proto.exchange(o, buf, packed));
   if (ev_b) PR_HIP(hipEventRecord(ev_b, g->xstream));
   g->x_pending = true;
-  return PR_OK;
+  return bound_lead(g, g->ipc);
 }
 
 // Destroy: the peers may still be copying out of this rank's send buffers; wait for the copies of

@@ -418,6 +418,15 @@ __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs)
 #ifndef PR_GATHER_AUX
 #define PR_GATHER_AUX 0
 #endif
+// Attribution ladder of k_spmv_hot (A/B builds only, compact codes; 0 = the product):
+//   1 every gather out of range (no cold gather; same instructions)   [wrong ranks]
+//   2 no gather instructions at all (values from LDS only)           [wrong ranks]
+//   3 one extra all-out-of-range gather per entry (TA cost of an idle gather instruction)
+//   4 no partial-slot stores (the reduce still runs)                  [wrong ranks]
+//   5 a gather instruction is skipped when no lane of the wave has a cold entry there
+#ifndef PR_HOT_DIAG
+#define PR_HOT_DIAG 0
+#endif
 
 // The unit's values: per entry an LDS read (hot) and a range-checked gather-space load (cold),
 // one of them an exact 0.
@@ -444,7 +453,22 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+#if PR_HOT_DIAG == 0 || PR_HOT_DIAG == 4
     const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, PR_GATHER_AUX));
+#elif PR_HOT_DIAG == 1
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs) | kEntGlobal, 0, PR_GATHER_AUX));
+#elif PR_HOT_DIAG == 2
+    const double b = 0.0;
+#elif PR_HOT_DIAG == 3
+    const uint32_t off = cold_offset<PIECE>(b8, cs);
+    const double b = __dadd_rn(__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off, 0, PR_GATHER_AUX)),
+                               __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off | kEntGlobal, 0, PR_GATHER_AUX)));
+#elif PR_HOT_DIAG == 5
+    const uint32_t off = cold_offset<PIECE>(b8, cs);
+    double b = 0.0;
+    if (__builtin_amdgcn_ballot_w64((int32_t)off >= 0))
+      b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off, 0, PR_GATHER_AUX));
+#endif
     v[j] = __dadd_rn(a, b);
   }
 }
@@ -536,6 +560,9 @@ __device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, con
     const int n = min(kStageSlots, nseg - base);
     const int i2 = 2 * lane_id();
     const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
+#if PR_HOT_DIAG == 4
+    if (u.r0 != 0x7FFFFFFF) continue;  // never false: the stores are skipped, the reduce is kept
+#endif
     if (i2 + 1 < n) {
       const pr_v4i q = *reinterpret_cast<const pr_v4i *>(stage + i2);
       __builtin_amdgcn_raw_buffer_store_b128(q, prs, o, 0, 2);

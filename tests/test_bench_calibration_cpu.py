@@ -35,13 +35,18 @@ class FakeGraph:
     def mode(self):
         if self.ipc:
             b = "blit_" if self.blit else ""
-            return (f"ipc_{b}chunked_early" if self.ipc == 2 else f"ipc_{b}chunked") if self.chunked else f"ipc_{b}unchunked"
+            if not self.chunked:
+                return f"ipc_{b}unchunked"
+            name = f"ipc_{b}chunked_early" if self.ipc == 2 else f"ipc_{b}chunked"
+            return name + (f"_reserve{self.reserve}" if self.reserve else "")
         return f"chunked_reserve{self.reserve}" if self.chunked else "unchunked"
 
     def set_exchange_ipc(self, on):
         self.switches.append(("ipc", on))
         if on and self.script.get("ipc_setup_fails"):
             raise RuntimeError("IPC exchange set-up failed on a peer")
+        if self.script.get("set_ipc_fails") == (self.rank, on):
+            raise RuntimeError("PR_OPT_XCHG_IPC: the ranks asked for different modes")
         if not on and self.script.get("switch_back_fails_on") == self.rank and self.stepped_ipc:
             raise RuntimeError("quiesce failed")
         self.ipc = on
@@ -147,7 +152,8 @@ def test_all_modes_agree_and_are_candidates():
     ov = r0["overlap"]
     assert r0["ipc_ok"] and "rejected" not in ov and "ipc_error" not in ov
     for name in ("unchunked", "chunked_reserve0", "chunked_reserve1", "chunked_reserve2", "ipc_unchunked",
-                 "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early"):
+                 "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early",
+                 "ipc_blit_chunked_early_reserve1", "ipc_blit_chunked_early_reserve2"):
         assert ov[f"{name}_ms_per_step"] > 0
     assert ov["candidates_bitwise_checked"] is True
 
@@ -235,4 +241,19 @@ def test_parity_leg_records_a_failing_mode_on_every_rank():
         assert v["failed"] == ["ipc_chunked"]
         assert v["checked"]["ipc_unchunked"] is True and v["checked"]["chunked_reserve0"] is True
         assert v["checked"]["ipc_blit_unchunked"] is False
+        assert v["final_ipc"] == 0
+
+
+def test_parity_leg_agrees_a_failed_switch_before_running_the_mode():
+    """switching to a mode that raises on ONE rank (here every per-chunk publication mode
+    on rank 1) is agreed before any rank runs the mode, so the ranks never pair one mode's reductions
+    with another's: the modes are recorded as failed on every rank, every other mode is still checked
+    bitwise on every rank, and every rank ends on the RCCL reference."""
+    res = _run({"set_ipc_fails": (1, 2), "timed": "ipc_unchunked"}, worker=_parity_worker)
+    early = sorted(m[0] for m in __import__("bench").IPC_MODES if m[3] == 2)
+    for v in res.values():
+        assert "error" not in v, v
+        assert v["failed"] == early
+        assert all(v["checked"][m] is True for m in ("ipc_unchunked", "ipc_chunked", "chunked_reserve0",
+                                                     "ipc_blit_unchunked"))
         assert v["final_ipc"] == 0

@@ -61,7 +61,8 @@ def _check_ipc(line):
     ab, par = line["exchange_overlap_ab"], line["parity"]
     assert "ipc_error" not in ab, ab.get("ipc_error")
     assert ab["candidates_bitwise_checked"] is True and not ab.get("rejected"), ab.get("rejected")
-    names = ("ipc_unchunked", "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early")
+    names = ("ipc_unchunked", "ipc_chunked", "ipc_chunked_early", "ipc_blit_unchunked", "ipc_blit_chunked_early",
+             "ipc_blit_chunked_early_reserve1", "ipc_blit_chunked_early_reserve2")
     for name in names:  # early: per-chunk publication of the send runs
         assert ab[f"{name}_ms_per_step"] > 0
         assert par[f"{name}_bitwise_equal_rccl"] is True
@@ -105,7 +106,8 @@ def test_rccl_exchange_on_shared_device(world, extra):
         assert ab is not None and ab["chosen"] in ("unchunked", "chunked_reserve0", "chunked_reserve1",
                                                    "chunked_reserve2", "ipc_unchunked", "ipc_chunked",
                                                    "ipc_chunked_early", "ipc_blit_unchunked",
-                                                   "ipc_blit_chunked_early")
+                                                   "ipc_blit_chunked_early", "ipc_blit_chunked_early_reserve1",
+                                                   "ipc_blit_chunked_early_reserve2")
         assert par["max_rel_overlapped_exchange"] <= RANK_TOL
         _check_ipc(line)
 
@@ -196,3 +198,29 @@ def test_ipc_modes_long_run_shared_device():
     errors = [r for r in steps if "error" in r]
     assert not errors, errors[:4]
     assert len(steps) == 2 * 32 and all(r["bitwise_equal_ref"] for r in steps)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(420)
+def test_ipc_one_long_step_shared_device():
+    """one pr_step of 300 iterations with no sync inside, in IPC mode 2 (per-chunk
+    publication, chunked copies; copy engines and blit) and mode 1, on two ranks sharing the device.
+    The host enqueues far ahead of its device there; the library bounds that lead (pr_ipc.hip
+    bound_lead) so no interprocess event generation is destroyed before the device has passed every
+    record and wait on it.  Every run must give bitwise the RCCL unchunked ranks of 300 iterations."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "tools", "ipc_modes_probe.py"),
+           "--rounds", "0", "--scale", "22", "--long", "300"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    recs, dec = [], json.JSONDecoder()
+    for line in p.stdout.splitlines():
+        i = line.find("{")
+        while i >= 0:
+            obj, end = dec.raw_decode(line, i)
+            recs.append(obj)
+            i = line.find("{", end)
+    longs = [r for r in recs if "long" in r]
+    assert p.returncode == 0 and longs, f"rc={p.returncode}\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    assert not [r for r in longs if "error" in r], longs
+    assert len(longs) == 2 * 3 and all(r["bitwise_equal_ref"] for r in longs)

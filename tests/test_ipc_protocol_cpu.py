@@ -28,6 +28,9 @@ def model():
     lib.ipc_model_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                   ctypes.c_char_p, ctypes.c_int]
     lib.ipc_model_run.restype = ctypes.c_int64
+    lib.ipc_model_run2.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_char_p, ctypes.c_int]
+    lib.ipc_model_run2.restype = ctypes.c_int64
     lib.ipc_model_chunk_end.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
     lib.ipc_model_chunk_end.restype = ctypes.c_int64
     return lib
@@ -49,6 +52,20 @@ def test_every_wait_binds_to_the_record_it_means(model, P, nc, n_ops, seed, dela
     waits = _run(model, P, n_ops, seed, delay_us, nc=nc)
     # every exchange waits on each peer's sent record, and every reuse of a buffer on each peer's
     # copied record of its previous exchange
+    assert waits >= n_ops * (P - 1)
+
+
+@pytest.mark.parametrize("P,nc,n_ops,seed,delay_us,reenable", [(2, 8, 700, 21, 0, 0), (3, 4, 500, 22, 5, 0),
+                                                               (2, 8, 600, 23, 5, 25), (4, 8, 400, 24, 5, 15),
+                                                               (8, 2, 300, 25, 3, 20)])
+def test_event_generations_past_the_runtime_limit(model, P, nc, n_ops, seed, delay_us, reenable):
+    """the event generations (csrc/pr_ipc_gens.h, the helper pr_ipc.hip uses) under the
+    checker -- runs far past 3 x 30 exchanges per buffer, optionally with re-enables (the counts
+    restart, a new epoch): no event takes more than the runtime's 32 records, and every wait picks,
+    by the library's rule, the generation whose latest record is the one meant."""
+    err = ctypes.create_string_buffer(512)
+    waits = model.ipc_model_run2(P, nc, n_ops, seed, delay_us, reenable, err, len(err))
+    assert waits >= 0, err.value.decode()
     assert waits >= n_ops * (P - 1)
 
 

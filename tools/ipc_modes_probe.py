@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 
 # (PR_OPT_XCHG_IPC, PR_OPT_XCHG_CHUNKS, PR_OPT_XCHG_IPC_BLIT)
+LONG_MODES = [(2, 1, 0), (1, 0, 0), (2, 1, 1)]
 SEQ = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (2, 1, 0), (2, 0, 0), (0, 1, 0), (1, 1, 1), (2, 1, 0), (1, 0, 1), (2, 1, 1),
        (0, 0, 0), (2, 1, 0), (2, 1, 1), (1, 1, 0), (1, 0, 0), (2, 1, 0)]
 
@@ -28,6 +29,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=1, help="repeat the switch sequence")
     ap.add_argument("--only", type=int, default=-1, help="run only this IPC mode (with chunks on), after the reference")
+    ap.add_argument("--long", type=int, default=0,
+                    help="then one pr_step of this many iterations with no sync inside, per mode of LONG_MODES, "
+                         "against the RCCL unchunked ranks of the same count (ADVICE r5: the host runs ahead)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     os.environ["NCCL_HOSTID"] = f"pr-probe-rank{rank}"
@@ -52,9 +56,9 @@ def main():
     dist.broadcast_object_list(obj, src=0)
     g.attach_comm(rank, world, obj[0])
 
-    def run():
+    def run(iters=None):
         g.reset()
-        g.step(a.iters)
+        g.step(a.iters if iters is None else iters)
         g.sync()
         out = np.zeros(V)
         g.ranks(out)
@@ -82,6 +86,24 @@ def main():
                 g.set_exchange_ipc(0)
             except Exception as e:  # noqa: BLE001
                 print(json.dumps({"rank": rank, "switch_back_error": str(e)}), flush=True)
+                break
+    if a.long > 0 and n_err == 0:
+        g.set_exchange_ipc(0)
+        g.set_exchange_ipc_blit(False)
+        g.set_exchange_chunks(False)
+        ref_long = run(a.long)
+        for ipc, chunks, blit in LONG_MODES:
+            rec = {"rank": rank, "long": a.long, "ipc": ipc, "chunks": chunks, "blit": blit}
+            try:
+                g.set_exchange_ipc(ipc)
+                g.set_exchange_ipc_blit(bool(blit))
+                g.set_exchange_chunks(bool(chunks))
+                rec["bitwise_equal_ref"] = bool(np.array_equal(run(a.long), ref_long))
+            except Exception as e:  # noqa: BLE001 -- reported
+                rec["error"] = str(e)
+                n_err += 1
+            print(json.dumps(rec), flush=True)
+            if "error" in rec:
                 break
     print(json.dumps({"rank": rank, "steps": len(seq), "errors": n_err}), flush=True)
     g.close()
