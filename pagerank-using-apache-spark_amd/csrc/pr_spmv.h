@@ -423,7 +423,7 @@ __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs)
 //   2 no gather instructions at all (values from LDS only)           [wrong ranks]
 //   3 one extra all-out-of-range gather per entry (TA cost of an idle gather instruction)
 //   4 no partial-slot stores (the reduce still runs)                  [wrong ranks]
-//   5 a gather instruction is skipped when no lane of the wave has a cold entry there
+// (profiles/r06/README.md: the measured ladder, and the variants measured and removed)
 #ifndef PR_HOT_DIAG
 #define PR_HOT_DIAG 0
 #endif
@@ -453,9 +453,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const uint32_t b8 = idx << 3;
     const uint32_t la = min(b8, cs.zb);  // hot: its slot; cold: the 0.0 slot
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
-#if PR_HOT_DIAG == 0 || PR_HOT_DIAG == 4
-    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, PR_GATHER_AUX));
-#elif PR_HOT_DIAG == 1
+#if PR_HOT_DIAG == 1
     const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs) | kEntGlobal, 0, PR_GATHER_AUX));
 #elif PR_HOT_DIAG == 2
     const double b = 0.0;
@@ -463,11 +461,8 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const uint32_t off = cold_offset<PIECE>(b8, cs);
     const double b = __dadd_rn(__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off, 0, PR_GATHER_AUX)),
                                __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off | kEntGlobal, 0, PR_GATHER_AUX)));
-#elif PR_HOT_DIAG == 5
-    const uint32_t off = cold_offset<PIECE>(b8, cs);
-    double b = 0.0;
-    if (__builtin_amdgcn_ballot_w64((int32_t)off >= 0))
-      b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, off, 0, PR_GATHER_AUX));
+#else
+    const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs), 0, PR_GATHER_AUX));
 #endif
     v[j] = __dadd_rn(a, b);
   }
@@ -533,30 +528,43 @@ __device__ __forceinline__ void stage_segment_sums(const LaneMeta &m, const doub
   if (m.endm != 0u && e0 >= 0 && e0 < kStageSlots) stage[e0] = __dadd_rn(carry, stage[e0]);
 }
 
+
+// A STREAM unit's segment sums, held in registers until they are stored (wave_unit_store).
+struct UnitSums {
+  LaneMeta m;
+  double sv[kWavePT];
+  double carry;
+};
+
+// The sums of one unit: a PIECE is summed and written here (false); a STREAM unit's segment sums go
+// to `r` (true).
 template <class WC>
-__device__ __forceinline__ void wave_unit_reduce(const Unit &u, const WC &w, const double (&v)[kWavePT],
-                                                 __amdgpu_buffer_rsrc_t prs, double *__restrict__ piece_part,
-                                                 double *stage) {
+__device__ __forceinline__ bool wave_unit_sums(const Unit &u, const WC &w, const double (&v)[kWavePT],
+                                               double *__restrict__ piece_part, UnitSums &r) {
   if (u.meta < 0) {  // PIECE of a long segment
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) acc = __dadd_rn(acc, v[j]);
     acc = wave_sum(acc);
     if (lane_id() == 0) piece_part[-u.meta - 1] = acc;
-    return;
+    return false;
   }
-  const LaneMeta m = derive_meta(end_marks(w));
-  double sv[kWavePT], carry;
-  wave_segmented_sums(m, v, sv, &carry);
-  // the sums are staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced
-  // stores: two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an
-  // odd last slot alone -- half the store instructions of one 8-byte store per slot (-1.7 % at
-  // s26, profiles/r02/store_walk/).  Non-temporal: the partials are read back by the epilogue
-  // only after every class has run, so they should not evict the class region from L2.
+  r.m = derive_meta(end_marks(w));
+  wave_segmented_sums(r.m, v, r.sv, &r.carry);
+  return true;
+}
+
+// The sums are staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced
+// stores: two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an
+// odd last slot alone -- half the store instructions of one 8-byte store per slot (-1.7 % at
+// s26, profiles/r02/store_walk/).  Non-temporal: the partials are read back by the epilogue
+// only after every class has run, so they should not evict the class region from L2.
+__device__ __forceinline__ void wave_unit_store(const Unit &u, const UnitSums &r, __amdgpu_buffer_rsrc_t prs,
+                                                double *stage) {
   const int nseg = u.meta;
   static_assert(kStageSlots <= 2 * kWave, "one b128 pass");
   for (int base = 0; base < nseg; base += kStageSlots) {
-    stage_segment_sums(m, sv, carry, base, stage);
+    stage_segment_sums(r.m, r.sv, r.carry, base, stage);
     const int n = min(kStageSlots, nseg - base);
     const int i2 = 2 * lane_id();
     const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
@@ -629,10 +637,13 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   const int64_t stride = (int64_t)nteams * kWaves;
   uint32_t *ctr = reinterpret_cast<uint32_t *>(const_cast<double *>(hot) + hg.ctr_slot());
   const int lane = lane_id();
-  auto take = [&]() -> int64_t {
+  auto counter = [&]() -> uint32_t {
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(ctr, 1u);
-    t = (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+    return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+  };
+  auto take = [&]() -> int64_t {
+    const uint32_t t = counter();
     return beg + (int64_t)team * kWaves + (int64_t)(t % kWaves) + (int64_t)(t / kWaves) * stride;
   };
   int64_t k = take();
@@ -663,7 +674,9 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       unit_codes<CODE>(u[s2], cd, wc[s2]);
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/)
-      wave_unit_reduce(u[sl], wc[sl], v[sl], prs, piece_part, stage);
+      UnitSums us;
+      const bool stream = wave_unit_sums(u[sl], wc[sl], v[sl], piece_part, us);
+      if (stream) wave_unit_store(u[sl], us, prs, stage);
       // piece codes look their table delta up here; reading them before the reduce instead
       // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
       wave_unit_gather<code_is_piece(CODE)>(wc[s1], hot, cs, v[s1]);
@@ -884,6 +897,10 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
   const int nb = (int)min((int64_t)G, a.nblk - b0);
   uint32_t mw[MW][G], info[G];
   double rold[G], S[G];
+  double cnv[G];    // c' per block, for the fused pack
+  uint32_t pmv[G];  // the peers that read the row, per block
+#pragma unroll
+  for (int g = 0; g < G; ++g) pmv[g] = (pd.P > 1 && g < nb) ? a.pmask[(b0 + g) * kWave + lane] : 0u;
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int64_t L = (b0 + g) * kWave + lane;
@@ -1048,15 +1065,32 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
       }
       l1p = __dadd_rn(l1p, fabs(rn - rold[g]));
     }
-    if (pd.P > 1 && g < nb) {  // fused pack: c' into the send run of every peer that reads the row
-      const uint32_t pm = a.pmask[L];
-      const int64_t sb = (b0 + g) * pd.P;
-      for (int q = 0; q < pd.P; ++q) {
-        const bool has = (pm >> q) & 1u;
+    cnv[g] = cn;
+  }
+  // fused pack (P = 2...8): per peer q the group's rows that q reads form ONE run of its send buffer
+  // (consecutive from sbase[b0][q]); their c' are gathered in the (now free) LDS window in run order
+  // and leave as 16-byte stores through a descriptor ending at the run's end (the range check drops
+  // an odd last half) -- a few full-width stores per peer instead of one ballot store per block and
+  // peer (s26 P = 8 part: epilogue 109 -> 100 us, profiles/r06/README.md)
+  if (pd.P > 1) {
+    const int64_t sb0 = b0 * pd.P;
+    for (int q = 0; q < pd.P; ++q) {
+      int run = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const bool has = (pmv[g] >> q) & 1u;
         const unsigned long long bal = __ballot(has);
-        if (bal == 0ull) continue;
-        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        if (has) pd.sbuf[pd.soff[q] + a.sbase[sb + q] + k] = cn;
+        const int k = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, (uint32_t)run));
+        if (has) win[k] = cnv[g];
+        run += __popcll(bal);
+      }
+      if (run == 0) continue;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(pd.sbuf + pd.soff[q] + a.sbase[sb0 + q]), 0, (uint32_t)run * 8u, 0x00020000);
+      for (int o = 0; o < run; o += 2 * kWave) {
+        const int i = o + 2 * lane;
+        if (i < run)
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const pr_v4i *>(win + i), rs, (uint32_t)i * 8u, 0, 0);
       }
     }
   }
