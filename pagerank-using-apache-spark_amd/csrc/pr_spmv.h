@@ -423,6 +423,8 @@ __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs)
 //   2 no gather instructions at all (values from LDS only)           [wrong ranks]
 //   3 one extra all-out-of-range gather per entry (TA cost of an idle gather instruction)
 //   4 no partial-slot stores (the reduce still runs)                  [wrong ranks]
+//   5 the hot set is loaded in the first phase only (stale values after) [wrong ranks]
+//   6 = 2 + 4: no gather instructions and no partial-slot stores          [wrong ranks]
 // (profiles/r06/README.md: the measured ladder, and the variants measured and removed)
 #ifndef PR_HOT_DIAG
 #define PR_HOT_DIAG 0
@@ -455,7 +457,7 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
     const double a = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
 #if PR_HOT_DIAG == 1
     const double b = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, cold_offset<PIECE>(b8, cs) | kEntGlobal, 0, PR_GATHER_AUX));
-#elif PR_HOT_DIAG == 2
+#elif PR_HOT_DIAG == 2 || PR_HOT_DIAG == 6
     const double b = 0.0;
 #elif PR_HOT_DIAG == 3
     const uint32_t off = cold_offset<PIECE>(b8, cs);
@@ -568,7 +570,7 @@ __device__ __forceinline__ void wave_unit_store(const Unit &u, const UnitSums &r
     const int n = min(kStageSlots, nseg - base);
     const int i2 = 2 * lane_id();
     const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
-#if PR_HOT_DIAG == 4
+#if PR_HOT_DIAG == 4 || PR_HOT_DIAG == 6
     if (u.r0 != 0x7FFFFFFF) continue;  // never false: the stores are skipped, the reduce is kept
 #endif
     if (i2 + 1 < n) {
@@ -701,8 +703,10 @@ __device__ __forceinline__ void stage_hot_set(const HotGeom &hg, int x, const in
   const int nh = hg.P * hg.Kp;
   const int32_t *hp = hpos + (int64_t)x * nh;
   const double *reg = cin + (int64_t)x * hg.Q_pad;
+  // ladder 5: only the first phase loads its hot set (the rest keep stale values)
+  const bool load = PR_HOT_DIAG != 5 || x < kXcds;
   constexpr int kSB = 6;  // elements per thread in flight (3 batches cover 18429 slots)
-  for (int b0 = 0; b0 < nh; b0 += kSB * kHotThreads) {
+  for (int b0 = 0; load && b0 < nh; b0 += kSB * kHotThreads) {
     int32_t pos[kSB];
     double val[kSB];
     if constexpr (CONTIG) {
