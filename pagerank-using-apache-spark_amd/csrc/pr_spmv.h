@@ -470,6 +470,83 @@ __device__ __forceinline__ void wave_unit_gather(const WaveCodesC20 &w, const do
   }
 }
 
+// Entry j of a lane: its LDS hot-set byte address (cold entries: the 0.0 slot) and its gather-space
+// byte offset (hot and padding entries: >= 2^31, out of range).
+template <bool PIECE>
+__device__ __forceinline__ void entry_addr(const WaveCodes &w, int j, const ClassSrc &, uint32_t &la, uint32_t &go) {
+  const uint32_t c = w.c[j] & ~1u;  // bit 0: segment end mark
+  la = (int32_t)c < 0 ? 0u : c;
+  go = c ^ kEntGlobal;
+}
+template <bool PIECE>
+__device__ __forceinline__ void entry_addr(const WaveCodesC20 &w, int j, const ClassSrc &cs, uint32_t &la, uint32_t &go) {
+  const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
+  const uint32_t b8 = (lo | (((w.s >> (8 + 3 * j)) & 7u) << 16)) << 3;
+  la = min(b8, cs.zb);
+  go = cold_offset<PIECE>(b8, cs);
+}
+template <bool PIECE>
+__device__ __forceinline__ void entry_addr(const WaveCodesC24 &w, int j, const ClassSrc &cs, uint32_t &la, uint32_t &go) {
+  const uint32_t lo = (j & 1) ? (w.w[j >> 1] >> 16) : (w.w[j >> 1] & 0xFFFFu);
+  const uint32_t b8 = (lo | ((uint32_t)(w.s >> (8 + 4 * j)) & 15u) << 16) << 3;
+  la = min(b8, cs.zb);
+  go = cold_offset<PIECE>(b8, cs);
+}
+
+// The product's gathers (round 6): a unit's cold entries are gathered by dense instructions.  Every
+// lane finds its cold entries' ranks (a wave scan of the per-lane counts), their offsets go
+// through the wave's LDS window (128 at a time), each buffer load takes 64 of them, and the values
+// come back through the window to the lanes that own them: ceil(cold / 64) gather instructions per
+// unit instead of one per entry position (8), whose hot lanes were out of range -- an idle gather
+// instruction costs ~24 us per pass at R-MAT s26 (profiles/r06/README.md §1).  R-MAT s26 -2.5 %
+// per pass, Twitter shape -1.0 %, ER s24 -0.5 %, LiveJournal shape +0.7 %, s26 P = 8 parts
+// unchanged (profiles/r06/README.md §6).  v[j] is bitwise the per-position a + b (one of them an
+// exact zero).  The ladder builds (PR_HOT_DIAG) keep the per-position gathers above.
+static_assert(kStageSlots >= 2 * kWave, "the compact gather window holds 128 values");
+template <bool PIECE, class WC>
+__device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const double *hot, const ClassSrc &cs,
+                                                         double (&v)[kWavePT], double *win) {
+  uint32_t off[kWavePT];
+  uint32_t coldm = 0u;
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) {
+    uint32_t la;
+    entry_addr<PIECE>(w, j, cs, la, off[j]);
+    v[j] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    coldm |= ((int32_t)off[j] >= 0 ? 1u : 0u) << j;
+  }
+  const int cnt = __builtin_popcount(coldm);
+  const int incl = wave_incl_scan_i32(cnt);
+  const int excl = incl - cnt, total = __builtin_amdgcn_readlane(incl, kWave - 1);
+  const int lane = lane_id();
+  uint32_t *win32 = reinterpret_cast<uint32_t *>(win);
+  for (int base = 0; base < total; base += 2 * kWave) {  // rounds of 128 cold entries (the window)
+    int rk = excl - base;
+#pragma unroll
+    for (int j = 0; j < kWavePT; ++j) {
+      const bool c = (coldm >> j) & 1u;
+      if (c && rk >= 0 && rk < 2 * kWave) win32[rk] = off[j];
+      rk += c ? 1 : 0;
+    }
+    const int n = min(2 * kWave, total - base);
+    const uint32_t a0 = lane < n ? win32[lane] : kEntGlobal;
+    const uint32_t a1 = lane + kWave < n ? win32[lane + kWave] : kEntGlobal;
+    const double g0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a0, 0, PR_GATHER_AUX));
+    if (n > kWave) {  // a second instruction only when the round has more than 64 cold entries
+      const double g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
+      win[lane + kWave] = g1;
+    }
+    win[lane] = g0;  // the offsets are in a0 / a1 already (the wave's LDS accesses run in order)
+    rk = excl - base;
+#pragma unroll
+    for (int j = 0; j < kWavePT; ++j) {
+      const bool c = (coldm >> j) & 1u;
+      if (c && rk >= 0 && rk < 2 * kWave) v[j] = win[rk];
+      rk += c ? 1 : 0;
+    }
+  }
+}
+
 template <bool PIECE>
 __device__ __forceinline__ void wave_unit_gather(const WaveCodesC24 &w, const double *hot, const ClassSrc &cs,
                                                  double (&v)[kWavePT]) {
@@ -617,6 +694,19 @@ __device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typ
   else wave_unit_codes(u, static_cast<const uint32_t *>(cd.codes), w);
 }
 
+// A unit's values: dense cold gathers (the product), or one gather per entry position (the ladder
+// builds, PR_HOT_DIAG, as measured in profiles/r06/README.md §1).
+template <int CODE>
+__device__ __forceinline__ void unit_gather(const typename CodeOf<CODE>::T &w, const double *hot, const ClassSrc &cs,
+                                            double (&v)[kWavePT], double *win) {
+#if PR_HOT_DIAG
+  (void)win;
+  wave_unit_gather<code_is_piece(CODE)>(w, hot, cs, v);
+#else
+  wave_unit_gather_compact<code_is_piece(CODE)>(w, hot, cs, v, win);
+#endif
+}
+
 // One class's wave units with the class's hot set already in LDS.  The class's unit list is
 // dealt to the XCD's `nteams` workgroups in slices of kWaves consecutive units every
 // nteams * kWaves (this one is `team`; the slice rotates with the phase, so a workgroup on a
@@ -666,7 +756,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   unit_codes<CODE>(u[0], cd, wc[0]);
   u[1] = unit_at(k1 < end ? k1 : none_k);
   unit_codes<CODE>(u[1], cd, wc[1]);
-  wave_unit_gather<code_is_piece(CODE)>(wc[0], hot, cs, v[0]);
+  unit_gather<CODE>(wc[0], hot, cs, v[0], stage);
   while (true) {
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl) {
@@ -681,7 +771,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       if (stream) wave_unit_store(u[sl], us, prs, stage);
       // piece codes look their table delta up here; reading them before the reduce instead
       // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
-      wave_unit_gather<code_is_piece(CODE)>(wc[s1], hot, cs, v[s1]);
+      unit_gather<CODE>(wc[s1], hot, cs, v[s1], stage);
       k = k1;
       k1 = k2;
       if (k >= end) return;
