@@ -506,15 +506,17 @@ static_assert(kStageSlots >= 2 * kWave, "the compact gather window holds 128 val
 template <bool PIECE, class WC>
 __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const double *hot, const ClassSrc &cs,
                                                          double (&v)[kWavePT], double *win) {
-  uint32_t off[kWavePT];
+  uint32_t off[kWavePT], la[kWavePT];
   uint32_t coldm = 0u;
 #pragma unroll
   for (int j = 0; j < kWavePT; ++j) {
-    uint32_t la;
-    entry_addr<PIECE>(w, j, cs, la, off[j]);
-    v[j] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la);
+    entry_addr<PIECE>(w, j, cs, la[j], off[j]);
     coldm |= ((int32_t)off[j] >= 0 ? 1u : 0u) << j;
   }
+  // the hot-set reads first: issued after the first round's gathers instead they cost +4.5 % (the
+  // round's value write-back then queues behind them, profiles/r06/README.md §6)
+#pragma unroll
+  for (int j = 0; j < kWavePT; ++j) v[j] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(hot) + la[j]);
   const int cnt = __builtin_popcount(coldm);
   const int incl = wave_incl_scan_i32(cnt);
   const int excl = incl - cnt, total = __builtin_amdgcn_readlane(incl, kWave - 1);
@@ -532,11 +534,11 @@ __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const doub
     const uint32_t a0 = lane < n ? win32[lane] : kEntGlobal;
     const uint32_t a1 = lane + kWave < n ? win32[lane + kWave] : kEntGlobal;
     const double g0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a0, 0, PR_GATHER_AUX));
-    if (n > kWave) {  // a second instruction only when the round has more than 64 cold entries
-      const double g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
-      win[lane + kWave] = g1;
-    }
+    double g1 = 0.0;
+    if (n > kWave)  // a second instruction only when the round has more than 64 cold entries
+      g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
     win[lane] = g0;  // the offsets are in a0 / a1 already (the wave's LDS accesses run in order)
+    if (n > kWave) win[lane + kWave] = g1;
     rk = excl - base;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) {
