@@ -180,11 +180,16 @@ int prepare_hot_kernel() {
         PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
-  for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P>)})
+  for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P, false>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P, true>),
+                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P, true>)})
     PR_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
   return PR_OK;
 }
@@ -315,14 +320,25 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
   return PR_OK;
 }
 
+// Dense cold gathers (pr_spmv.h unit_gather) once a pass has this many wave units per CU: R-MAT s26
+// (8.8 K per CU) -2.5 %, ER s24 (2 K) -0.5 %; below it a unit's latency chain matters more than its
+// gather instructions (R-MAT s20, 0.12 K: +11 %; LiveJournal shape, 0.5 K: +0.7 %).
+constexpr int64_t kDenseUnitsPerCU = 1024;
+template <bool DENSE>
+void *hot_kernel(int code) {
+  return code == kCodeC20    ? reinterpret_cast<void *>(k_spmv_hot<kCodeC20, DENSE>)
+         : code == kCodeC24  ? reinterpret_cast<void *>(k_spmv_hot<kCodeC24, DENSE>)
+         : code == kCodeC20P ? reinterpret_cast<void *>(k_spmv_hot<kCodeC20P, DENSE>)
+         : code == kCodeC24P ? reinterpret_cast<void *>(k_spmv_hot<kCodeC24P, DENSE>)
+                             : reinterpret_cast<void *>(k_spmv_hot<kCodeU32, DENSE>);
+}
+
 int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   if (ph1 < 0) ph1 = n_hot_phases(g);
   const CodeSrc cd{g->colh.p, g->cside.as<uint32_t>()};
-  auto kern = g->code == kCodeC20    ? k_spmv_hot<kCodeC20>
-              : g->code == kCodeC24  ? k_spmv_hot<kCodeC24>
-              : g->code == kCodeC20P ? k_spmv_hot<kCodeC20P>
-              : g->code == kCodeC24P ? k_spmv_hot<kCodeC24P>
-                                     : k_spmv_hot<kCodeU32>;
+  const bool dense = g->n_hunits >= kDenseUnitsPerCU * (int64_t)g->hot_grid_full;
+  auto kern = reinterpret_cast<decltype(&k_spmv_hot<kCodeU32, false>)>(dense ? hot_kernel<true>(g->code)
+                                                                              : hot_kernel<false>(g->code));
   hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),

@@ -696,17 +696,19 @@ __device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typ
   else wave_unit_codes(u, static_cast<const uint32_t *>(cd.codes), w);
 }
 
-// A unit's values: dense cold gathers (the product), or one gather per entry position (the ladder
-// builds, PR_HOT_DIAG, as measured in profiles/r06/README.md §1).
-template <int CODE>
+// A unit's values: dense cold gathers (DENSE: many units per CU), or one gather instruction per
+// entry position (small passes, where a unit's chain latency matters more than its instruction
+// count: R-MAT s20 +11 % with dense gathers, LiveJournal shape +0.7 %; and the ladder builds,
+// PR_HOT_DIAG, as measured in profiles/r06/README.md §1).
+template <int CODE, bool DENSE>
 __device__ __forceinline__ void unit_gather(const typename CodeOf<CODE>::T &w, const double *hot, const ClassSrc &cs,
                                             double (&v)[kWavePT], double *win) {
-#if PR_HOT_DIAG
-  (void)win;
-  wave_unit_gather<code_is_piece(CODE)>(w, hot, cs, v);
-#else
-  wave_unit_gather_compact<code_is_piece(CODE)>(w, hot, cs, v, win);
-#endif
+  if constexpr (DENSE && !PR_HOT_DIAG) {
+    wave_unit_gather_compact<code_is_piece(CODE)>(w, hot, cs, v, win);
+  } else {
+    (void)win;
+    wave_unit_gather<code_is_piece(CODE)>(w, hot, cs, v);
+  }
 }
 
 // One class's wave units with the class's hot set already in LDS.  The class's unit list is
@@ -716,7 +718,7 @@ __device__ __forceinline__ void unit_gather(const typename CodeOf<CODE>::T &w, c
 // take its units in order from a counter in a spare LDS word (zeroed before the class), so a slow
 // wave takes fewer and the waves reach the class's end together (-3.5 % at s26 against a static
 // interleave, profiles/r02/assign_lds_ab/).
-template <int CODE>
+template <int CODE, bool DENSE>
 __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, const Unit *__restrict__ units,
                                                 const int64_t *__restrict__ ucum, const HotGeom &hg,
                                                 const CodeSrc &cd, const double *hot, const ClassSrc &cs,
@@ -758,7 +760,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
   unit_codes<CODE>(u[0], cd, wc[0]);
   u[1] = unit_at(k1 < end ? k1 : none_k);
   unit_codes<CODE>(u[1], cd, wc[1]);
-  unit_gather<CODE>(wc[0], hot, cs, v[0], stage);
+  unit_gather<CODE, DENSE>(wc[0], hot, cs, v[0], stage);
   while (true) {
 #pragma unroll
     for (int sl = 0; sl < 3; ++sl) {
@@ -773,7 +775,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       if (stream) wave_unit_store(u[sl], us, prs, stage);
       // piece codes look their table delta up here; reading them before the reduce instead
       // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
-      unit_gather<CODE>(wc[s1], hot, cs, v[s1], stage);
+      unit_gather<CODE, DENSE>(wc[s1], hot, cs, v[s1], stage);
       k = k1;
       k1 = k2;
       if (k >= end) return;
@@ -837,7 +839,7 @@ __device__ __forceinline__ void stage_hot_set(const HotGeom &hg, int x, const in
 // (phases [ph0, ph1): one launch per phase when the exchange overlaps), restaging the hot set
 // per class.  CODE: the entry code format (pr_internal.h); compact codes address class x's
 // region of the gather space [x*Q_pad, (x+1)*Q_pad) (P = 1 only).
-template <int CODE>
+template <int CODE, bool DENSE>
 __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict__ units,
                                                           const int64_t *__restrict__ ucum, HotGeom hg,
                                                           CodeSrc cd, const double *__restrict__ cin,
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
     if (ph > ph0) __syncthreads();  // every wave is done with the previous class's hot set
     stage_hot_set<kPiece, CODE == kCodeC20 || CODE == kCodeC24>(hg, x, hpos, ptab, cin, hot, tblw);
     __syncthreads();
-    hot_class_units<CODE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
+    hot_class_units<CODE, DENSE>(x, team, nteams, units, ucum, hg, cd, hot, cs, partial, poff, piece_part, stage);
   }
 }
 
