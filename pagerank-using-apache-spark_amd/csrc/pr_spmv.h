@@ -33,6 +33,12 @@ __device__ __forceinline__ double affine(double S, double tdc, double teleport, 
 
 typedef int pr_v4i __attribute__((ext_vector_type(4)));
 typedef int pr_v2i __attribute__((ext_vector_type(2)));
+// LDS windows are written as doubles and read back as 16-byte int vectors (or written as u32
+// offsets and then as doubles, wave_unit_gather_compact): these access types alias anything, so
+// type-based alias analysis can never reorder such accesses of one window against each other.
+typedef pr_v4i pr_v4i_alias __attribute__((may_alias));
+typedef uint32_t pr_u32_alias __attribute__((may_alias));
+typedef double pr_f64_alias __attribute__((may_alias));
 
 template <int PT, bool NT>
 __device__ __forceinline__ void load_cols(const int32_t *__restrict__ p, int32_t (&ci)[PT]) {
@@ -521,7 +527,8 @@ __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const doub
   const int incl = wave_incl_scan_i32(cnt);
   const int excl = incl - cnt, total = __builtin_amdgcn_readlane(incl, kWave - 1);
   const int lane = lane_id();
-  uint32_t *win32 = reinterpret_cast<uint32_t *>(win);
+  pr_u32_alias *win32 = reinterpret_cast<pr_u32_alias *>(win);
+  pr_f64_alias *winf = reinterpret_cast<pr_f64_alias *>(win);
   for (int base = 0; base < total; base += 2 * kWave) {  // rounds of 128 cold entries (the window)
     int rk = excl - base;
 #pragma unroll
@@ -537,13 +544,13 @@ __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const doub
     double g1 = 0.0;
     if (n > kWave)  // a second instruction only when the round has more than 64 cold entries
       g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
-    win[lane] = g0;  // the offsets are in a0 / a1 already (the wave's LDS accesses run in order)
-    if (n > kWave) win[lane + kWave] = g1;
+    winf[lane] = g0;  // the offsets are in a0 / a1 already (the wave's LDS accesses run in order)
+    if (n > kWave) winf[lane + kWave] = g1;
     rk = excl - base;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) {
       const bool c = (coldm >> j) & 1u;
-      if (c && rk >= 0 && rk < 2 * kWave) v[j] = win[rk];
+      if (c && rk >= 0 && rk < 2 * kWave) v[j] = winf[rk];
       rk += c ? 1 : 0;
     }
   }
@@ -653,7 +660,7 @@ __device__ __forceinline__ void wave_unit_store(const Unit &u, const UnitSums &r
     if (u.r0 != 0x7FFFFFFF) continue;  // never false: the stores are skipped, the reduce is kept
 #endif
     if (i2 + 1 < n) {
-      const pr_v4i q = *reinterpret_cast<const pr_v4i *>(stage + i2);
+      const pr_v4i q = *reinterpret_cast<const pr_v4i_alias *>(stage + i2);
       __builtin_amdgcn_raw_buffer_store_b128(q, prs, o, 0, 2);
     } else if (i2 < n) {
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i2]), prs, o, 0, 2);
@@ -1188,7 +1195,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
       for (int o = 0; o < run; o += 2 * kWave) {
         const int i = o + 2 * lane;
         if (i < run)
-          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const pr_v4i *>(win + i), rs, (uint32_t)i * 8u, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const pr_v4i_alias *>(win + i), rs, (uint32_t)i * 8u, 0, 0);
       }
     }
   }
