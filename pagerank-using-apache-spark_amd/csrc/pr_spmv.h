@@ -1177,6 +1177,7 @@ __device__ __forceinline__ void epi_group(const EpiArgs &a, const PackDst &pd, i
   // and leave as 16-byte stores through a descriptor ending at the run's end (the range check drops
   // an odd last half) -- a few full-width stores per peer instead of one ballot store per block and
   // peer (s26 P = 8 part: epilogue 109 -> 100 us, profiles/r06/README.md)
+  static_assert(G * kWave <= W, "a group's run for one peer fits the window");
   if (pd.P > 1) {
     const int64_t sb0 = b0 * pd.P;
     for (int q = 0; q < pd.P; ++q) {
