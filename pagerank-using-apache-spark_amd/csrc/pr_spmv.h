@@ -643,28 +643,28 @@ __device__ __forceinline__ bool wave_unit_sums(const Unit &u, const WC &w, const
 }
 
 // The sums are staged in the wave's LDS window (kStageSlots at a time) and leave as coalesced
-// stores: two slots per lane in one 16-byte non-temporal store (dword alignment is enough), an
-// odd last slot alone -- half the store instructions of one 8-byte store per slot (-1.7 % at
-// s26, profiles/r02/store_walk/).  Non-temporal: the partials are read back by the epilogue
-// only after every class has run, so they should not evict the class region from L2.
-__device__ __forceinline__ void wave_unit_store(const Unit &u, const UnitSums &r, __amdgpu_buffer_rsrc_t prs,
-                                                double *stage) {
+// stores: two slots per lane in one 16-byte non-temporal store (dword alignment is enough; half
+// the store instructions of one 8-byte store per slot: -1.7 % at s26, profiles/r02/store_walk/),
+// through a descriptor of the unit's own slots, so an odd last slot rides a 16-byte store whose
+// second half the range check drops (it checks per dword; one store instruction per pass instead
+// of a 16-byte and an 8-byte one: -0.6 % at s26, profiles/r06/README.md §6).  Non-temporal: the
+// partials are read back by the epilogue only after every class has run, so they should not evict
+// the class region from L2.
+__device__ __forceinline__ void wave_unit_store(const Unit &u, const UnitSums &r, double *pcls, double *stage) {
   const int nseg = u.meta;
   static_assert(kStageSlots <= 2 * kWave, "one b128 pass");
+  const __amdgpu_buffer_rsrc_t urs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(pcls + u.r0), 0, (uint32_t)nseg * 8u, 0x00020000);
   for (int base = 0; base < nseg; base += kStageSlots) {
     stage_segment_sums(r.m, r.sv, r.carry, base, stage);
     const int n = min(kStageSlots, nseg - base);
     const int i2 = 2 * lane_id();
-    const uint32_t o = (uint32_t)(u.r0 + base + i2) * 8u;
 #if PR_HOT_DIAG == 4 || PR_HOT_DIAG == 6
     if (u.r0 != 0x7FFFFFFF) continue;  // never false: the stores are skipped, the reduce is kept
 #endif
-    if (i2 + 1 < n) {
-      const pr_v4i q = *reinterpret_cast<const pr_v4i_alias *>(stage + i2);
-      __builtin_amdgcn_raw_buffer_store_b128(q, prs, o, 0, 2);
-    } else if (i2 < n) {
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(pr_v2i, stage[i2]), prs, o, 0, 2);
-    }
+    if (i2 < n)
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const pr_v4i_alias *>(stage + i2), urs,
+                                             (uint32_t)(base + i2) * 8u, 0, 2);
   }
 }
 
@@ -732,8 +732,6 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
                                                 double *__restrict__ partial, const int64_t *__restrict__ poff,
                                                 double *__restrict__ piece_part, double *stage) {
   const int64_t p0 = poff[x];
-  const __amdgpu_buffer_rsrc_t prs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(partial + p0), 0, (uint32_t)((poff[x + 1] - p0) * 8), 0x00020000);
   const int64_t beg = ucum[x], end = ucum[x + 1];
   constexpr int kWaves = kHotThreads / kWave;
   team = (team + 5 * (x / kXcds)) % nteams;
@@ -779,7 +777,7 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       // -3.7 % at s26, profiles/r02/order_ab/)
       UnitSums us;
       const bool stream = wave_unit_sums(u[sl], wc[sl], v[sl], piece_part, us);
-      if (stream) wave_unit_store(u[sl], us, prs, stage);
+      if (stream) wave_unit_store(u[sl], us, partial + p0, stage);
       // piece codes look their table delta up here; reading them before the reduce instead
       // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
       unit_gather<CODE, DENSE>(wc[s1], hot, cs, v[s1], stage);
