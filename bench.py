@@ -838,9 +838,12 @@ def main() -> int:
                 # `achieved`; traffic_detail names the dominant kernel's own share
                 "traffic": (tr or {}).get("per_pass"),
                 "traffic_detail": tr,
-                "kernel": (f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue_grp (split layout, {info.get('classes')} "
-                           "column classes, run per XCD in phases)" if info.get("layout") == 1
-                           else "spmv pass: k_spmv_units (fused layout)"),
+                # one part: the whole iteration, timed as one interval over the K steps (no event
+                # between kernels: each is a ~5 us marker packet); parts: the pass's kernels only
+                "kernel": ((f"spmv pass: k_spmv_hot + k_seg_reduce + k_epilogue_grp (split layout, {info.get('classes')} "
+                            "column classes, run per XCD in phases)" if info.get("layout") == 1
+                            else "spmv pass: k_spmv_units (fused layout)")
+                           + (" + k_finalize: the whole iteration" if world == 1 else "")),
                 "classes": info.get("classes"),
                 "bytes_model": "12*E'_part + 36*V_part per launch (pull-fp64-v1)",
                 "spmv_ms_mean": round(spmv_ms, 4),

@@ -82,7 +82,9 @@ extern "C" {
 #define PR_STAT_ITERS 0          /* iterations run since the last reset                     */
 #define PR_STAT_LAST_DC 1        /* danglingContrib used by the last iteration              */
 #define PR_STAT_LAST_L1 2        /* sum |r_k - r_{k-1}| of the last iteration                */
-#define PR_STAT_SPMV_MS_MEAN 3   /* mean HIP-event time of one SpMV pass, kernels only: exchange waits excluded (timing on) */
+#define PR_STAT_SPMV_MS_MEAN 3   /* mean HIP-event time of one SpMV pass, kernels only: exchange waits excluded (timing on);
+                                    one part: the whole iteration (k_finalize included), one
+                                    interval per pr_step call with no event between kernels */
 #define PR_STAT_SPMV_LAUNCHES 4  /* SpMV passes timed */
 #define PR_STAT_ITER_MS_MEAN 5   /* mean HIP-event time of a whole iteration, its exchange
                                     included (timing on)                                    */

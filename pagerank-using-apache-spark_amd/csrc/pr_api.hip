@@ -363,8 +363,9 @@ int pr_get_stats(pr_graph *g, double *stats, int32_t n_stats) {
       acc += a > b ? a : b;
     }
     v[PR_STAT_ITER_MS_MEAN] = acc / (double)g->iter_ev.size();
-  } else {
+  } else {  // per interval: scaled to per iteration (one part: one interval per pr_step call)
     PR_TRY(mean_ms(g->iter_ev, &v[PR_STAT_ITER_MS_MEAN]));
+    if (g->iter_timed > 0) v[PR_STAT_ITER_MS_MEAN] *= (double)g->iter_ev.size() / (double)g->iter_timed;
   }
   v[PR_STAT_BUILD_MS] = g->build_ms;
   PR_TRY(mean_ms(g->xchg_ev, &v[PR_STAT_EXCHANGE_MS_MEAN]));
@@ -512,6 +513,7 @@ int pr_group_step(pr_graph *const *parts, int32_t n_parts, int32_t iterations) {
       int i1 = -1;
       PR_TRY(pr::time_mark(parts[p], parts[p]->stream, &i1));
       parts[p]->iter_ev.push_back({i0[p], i1});
+      ++parts[p]->iter_timed;
     }
   }
   return PR_OK;

@@ -128,9 +128,11 @@ struct pr_graph {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   // indices into ev_pool; spmv_ev holds one interval per pass, or one per hot phase (+ the rest of
-  // the pass) when the overlapped exchange gates the phases: spmv_passes passes in all
+  // the pass) when the overlapped exchange gates the phases, or (one part) one per pr_step call
+  // covering all its iterations: spmv_passes passes in all; iter_ev's intervals cover iter_timed
+  // iterations
   std::vector<std::pair<int, int>> spmv_ev, iter_ev, xchg_ev;
-  int64_t spmv_passes = 0;
+  int64_t spmv_passes = 0, iter_timed = 0;
   size_t ev_next = 0;
   // ev_pool index of an event recorded on `stream` with nothing enqueued after it yet, which the
   // next interval may start from instead of recording its own (-1: none); every record is a

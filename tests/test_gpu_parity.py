@@ -193,6 +193,8 @@ def test_step_api_and_stats(hip, oracle_c):
         with pytest.raises(hip.PageRankError):
             g.export_csr()
     assert st["iters"] == 7 and st["spmv_launches"] == 7 and st["spmv_ms_mean"] > 0
+    # one part: each pr_step call is one interval, scaled to per pass / per iteration alike
+    assert st["iter_ms_mean"] == pytest.approx(st["spmv_ms_mean"], rel=1e-9)
     assert abs(st["last_dc"] - ref["dc"][6]) <= 1e-9 * ref["dc"][6]
     assert abs(st["last_l1"] - ref["l1"][6]) <= 1e-9 * max(ref["l1"][6], 1)
     assert max_rel(r, ref["ranks"]) <= RANK_TOL
