@@ -1,3 +1,7 @@
+"""Per-iteration kernel times and the gaps between them from a rocprofv3 kernel trace of bench.py
+(one part): `python tools/iter_gaps.py <run_kernel_trace.csv>`.  Iterations are the kernels after
+the last k_reset, each ending with k_finalize; the first five are skipped.  Used for the timing-marker
+cost in DESIGN.md §6 (profiles/r06/coarse_timing/)."""
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
