@@ -501,14 +501,14 @@ __device__ __forceinline__ void entry_addr(const WaveCodesC24 &w, int j, const C
 
 // The product's gathers (round 6): a unit's cold entries are gathered by dense instructions.  Every
 // lane finds its cold entries' ranks (a wave scan of the per-lane counts), their offsets go
-// through the wave's LDS window (128 at a time), each buffer load takes 64 of them, and the values
+// through the wave's LDS window (256 at a time), each buffer load takes 64 of them, and the values
 // come back through the window to the lanes that own them: ceil(cold / 64) gather instructions per
 // unit instead of one per entry position (8), whose hot lanes were out of range -- an idle gather
 // instruction costs ~24 us per pass at R-MAT s26 (profiles/r06/README.md §1).  R-MAT s26 -2.5 %
 // per pass, Twitter shape -1.0 %, ER s24 -0.5 %, LiveJournal shape +0.7 %, s26 P = 8 parts
 // unchanged (profiles/r06/README.md §6).  v[j] is bitwise the per-position a + b (one of them an
 // exact zero).  The ladder builds (PR_HOT_DIAG) keep the per-position gathers above.
-static_assert(kStageSlots >= 2 * kWave, "the compact gather window holds 128 values");
+static_assert(kStageSlots >= 2 * kWave, "the compact gather window holds 128 values (256 offsets)");
 template <bool PIECE, class WC>
 __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const double *hot, const ClassSrc &cs,
                                                          double (&v)[kWavePT], double *win) {
@@ -529,29 +529,47 @@ __device__ __forceinline__ void wave_unit_gather_compact(const WC &w, const doub
   const int lane = lane_id();
   pr_u32_alias *win32 = reinterpret_cast<pr_u32_alias *>(win);
   pr_f64_alias *winf = reinterpret_cast<pr_f64_alias *>(win);
-  for (int base = 0; base < total; base += 2 * kWave) {  // rounds of 128 cold entries (the window)
+  // rounds of 256 cold entries (one round for most units at R-MAT s26): the window holds 256 u32 offsets,
+  // so up to four gather instructions are in flight at once, and their values come back through it
+  // in two halves of 128 (-0.8 % at s26 against rounds of 128 with two loads each, ER s24 the same:
+  // profiles/r06/dense/r6_wide/)
+  for (int base = 0; base < total; base += 4 * kWave) {
     int rk = excl - base;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) {
       const bool c = (coldm >> j) & 1u;
-      if (c && rk >= 0 && rk < 2 * kWave) win32[rk] = off[j];
+      if (c && (uint32_t)rk < (uint32_t)(4 * kWave)) win32[rk] = off[j];
       rk += c ? 1 : 0;
     }
-    const int n = min(2 * kWave, total - base);
+    const int n = min(4 * kWave, total - base);
     const uint32_t a0 = lane < n ? win32[lane] : kEntGlobal;
     const uint32_t a1 = lane + kWave < n ? win32[lane + kWave] : kEntGlobal;
+    const uint32_t a2 = lane + 2 * kWave < n ? win32[lane + 2 * kWave] : kEntGlobal;
+    const uint32_t a3 = lane + 3 * kWave < n ? win32[lane + 3 * kWave] : kEntGlobal;
     const double g0 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a0, 0, PR_GATHER_AUX));
-    double g1 = 0.0;
-    if (n > kWave)  // a second instruction only when the round has more than 64 cold entries
-      g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
-    winf[lane] = g0;  // the offsets are in a0 / a1 already (the wave's LDS accesses run in order)
+    double g1 = 0.0, g2 = 0.0, g3 = 0.0;  // a further instruction only for each further 64 entries
+    if (n > kWave) g1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a1, 0, PR_GATHER_AUX));
+    if (n > 2 * kWave) g2 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a2, 0, PR_GATHER_AUX));
+    if (n > 3 * kWave) g3 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(cs.crs, a3, 0, PR_GATHER_AUX));
+    winf[lane] = g0;  // the offsets are in a0..a3 already (the wave's LDS accesses run in order)
     if (n > kWave) winf[lane + kWave] = g1;
     rk = excl - base;
 #pragma unroll
     for (int j = 0; j < kWavePT; ++j) {
       const bool c = (coldm >> j) & 1u;
-      if (c && rk >= 0 && rk < 2 * kWave) v[j] = winf[rk];
+      if (c && (uint32_t)rk < (uint32_t)(2 * kWave)) v[j] = winf[rk];
       rk += c ? 1 : 0;
+    }
+    if (n > 2 * kWave) {  // the second half, after the first half's reads (in order, as above)
+      winf[lane] = g2;
+      if (n > 3 * kWave) winf[lane + kWave] = g3;
+      rk = excl - base - 2 * kWave;
+#pragma unroll
+      for (int j = 0; j < kWavePT; ++j) {
+        const bool c = (coldm >> j) & 1u;
+        if (c && (uint32_t)rk < (uint32_t)(2 * kWave)) v[j] = winf[rk];
+        rk += c ? 1 : 0;
+      }
     }
   }
 }
