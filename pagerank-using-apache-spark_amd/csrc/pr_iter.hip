@@ -322,7 +322,8 @@ int set_hot_reserve(pr_graph *g, int per_xcd) {
 
 // Dense cold gathers (pr_spmv.h unit_gather) once a pass has this many wave units per CU: R-MAT s26
 // (8.8 K per CU) -2.5 %, ER s24 (2 K) -0.5 %; below it a unit's latency chain matters more than its
-// gather instructions (R-MAT s20, 0.12 K: +11 %; LiveJournal shape, 0.5 K: +0.7 %).
+// gather instructions (R-MAT s20, 0.12 K: +11 %; LiveJournal shape, 0.5 K: +0.7 %; with the rounds of
+// 256 still +15 % / +0.4 %, profiles/r06/dense/r6_dense0/).
 constexpr int64_t kDenseUnitsPerCU = 1024;
 template <bool DENSE>
 void *hot_kernel(int code) {
