@@ -792,7 +792,8 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       u[s2] = unit_at(k2 < end ? k2 : none_k);
       unit_codes<CODE>(u[s2], cd, wc[s2]);
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
-      // -3.7 % at s26, profiles/r02/order_ab/)
+      // -3.7 % at s26, profiles/r02/order_ab/; with the dense gathers, issuing unit i+1's first
+      // round before unit i's sums and stores spilled 53 VGPRs at 4 waves per SIMD: not kept)
       UnitSums us;
       const bool stream = wave_unit_sums(u[sl], wc[sl], v[sl], piece_part, us);
       if (stream) wave_unit_store(u[sl], us, partial + p0, stage);
