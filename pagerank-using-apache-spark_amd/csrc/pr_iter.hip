@@ -180,17 +180,7 @@ int prepare_hot_kernel() {
         PR_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(epi_grp_kernel(c, walk, narrow)),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)epi_grp_lds(narrow)));
       }
-  for (const void *f : {reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P, false>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeU32, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC20P, true>),
-                        reinterpret_cast<const void *>(&k_spmv_hot<kCodeC24P, true>)})
-    PR_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes));
+  // k_spmv_hot holds its LDS statically (kHotLdsBytes): no dynamic-LDS attribute to raise
   return PR_OK;
 }
 
@@ -340,7 +330,8 @@ int launch_hot(pr_graph *g, int in, int ph0, int ph1) {
   const bool dense = g->n_hunits >= kDenseUnitsPerCU * (int64_t)g->hot_grid_full;
   auto kern = reinterpret_cast<decltype(&k_spmv_hot<kCodeU32, false>)>(dense ? hot_kernel<true>(g->code)
                                                                               : hot_kernel<false>(g->code));
-  hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), g->hot.lds_bytes(), g->stream,
+  if (g->hot.lds_bytes() > (size_t)kHotLdsBytes) return fail(PR_ERR_STATE, "hot set exceeds the LDS");
+  hipLaunchKernelGGL(kern, dim3((unsigned)g->hot_grid), dim3(kHotThreads), 0, g->stream,
                      g->hunits.as<Unit>(), g->hucum.as<int64_t>(), g->hot, cd, g->cbuf[in].as<double>(),
                      (uint32_t)(sizeof(double) * g->gsize), g->partial.as<double>(), g->poff.as<int64_t>(),
                      g->piece_part.as<double>(), g->hpos.as<int32_t>(), g->ptab.as<int32_t>(), ph0, ph1);

@@ -431,6 +431,7 @@ __device__ __forceinline__ uint32_t cold_offset(uint32_t b8, const ClassSrc &cs)
 //   4 no partial-slot stores (the reduce still runs)                  [wrong ranks]
 //   5 the hot set is loaded in the first phase only (stale values after) [wrong ranks]
 //   6 = 2 + 4: no gather instructions and no partial-slot stores          [wrong ranks]
+//   7 64 extra VALU instructions per unit (same results): is VALU on the critical path?
 // (profiles/r06/README.md: the measured ladder, and the variants measured and removed)
 #ifndef PR_HOT_DIAG
 #define PR_HOT_DIAG 0
@@ -728,7 +729,7 @@ __device__ __forceinline__ void unit_codes(const Unit &u, const CodeSrc &cd, typ
 template <int CODE, bool DENSE>
 __device__ __forceinline__ void unit_gather(const typename CodeOf<CODE>::T &w, const double *hot, const ClassSrc &cs,
                                             double (&v)[kWavePT], double *win) {
-  if constexpr (DENSE && !PR_HOT_DIAG) {
+  if constexpr (DENSE && (!PR_HOT_DIAG || PR_HOT_DIAG == 7)) {
     wave_unit_gather_compact<code_is_piece(CODE)>(w, hot, cs, v, win);
   } else {
     (void)win;
@@ -794,11 +795,21 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/; with the dense gathers, issuing unit i+1's first
       // round before unit i's sums and stores spilled 53 VGPRs at 4 waves per SIMD: not kept)
+#if PR_HOT_DIAG == 7
+      {  // ladder 7: 64 extra dependent VALU instructions per unit (is VALU on the critical path?)
+        uint32_t d = (uint32_t)lane;
+#pragma unroll
+        for (int q = 0; q < 64; ++q) asm volatile("v_add_u32 %0, %0, %1" : "+v"(d) : "v"((uint32_t)q));
+        if (d == 0xFFFFFFFFu) piece_part[0] = 0.0;  // never (keeps the chain)
+      }
+#endif
       UnitSums us;
       const bool stream = wave_unit_sums(u[sl], wc[sl], v[sl], piece_part, us);
       if (stream) wave_unit_store(u[sl], us, partial + p0, stage);
       // piece codes look their table delta up here; reading them before the reduce instead
       // measured the same (s26 P = 8 part 375 vs 371 us, profiles/r03/piece_codes/hoist_ab/)
+      // (unit i+2's codes issued after unit i+1's first gathers instead: +2..7 % at s26, the codes
+      // arrive later than the next decode needs them; profiles/r06/dense/r6_late/)
       unit_gather<CODE, DENSE>(wc[s1], hot, cs, v[s1], stage);
       k = k1;
       k1 = k2;
@@ -872,7 +883,7 @@ __global__ __launch_bounds__(kHotThreads) void k_spmv_hot(const Unit *__restrict
                                                           double *__restrict__ piece_part,
                                                           const int32_t *__restrict__ hpos,
                                                           const int32_t *__restrict__ ptab, int ph0, int ph1) {
-  extern __shared__ double hot[];
+  __shared__ double hot[kHotLdsBytes / sizeof(double)];  // static: LDS addresses fold into the instructions
   constexpr bool kPiece = code_is_piece(CODE);
   ClassSrc cs;
   cs.zb = (uint32_t)hg.slots() * 8u;
