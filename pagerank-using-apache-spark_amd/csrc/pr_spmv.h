@@ -794,7 +794,8 @@ __device__ __forceinline__ void hot_class_units(int x, int team, int nteams, con
       unit_codes<CODE>(u[s2], cd, wc[s2]);
       // reduce first: a gather issue stalled by a busy address unit cannot hold it up (ORDER 1:
       // -3.7 % at s26, profiles/r02/order_ab/; with the dense gathers, issuing unit i+1's first
-      // round before unit i's sums and stores spilled 53 VGPRs at 4 waves per SIMD: not kept)
+      // round before unit i's sums and stores spilled 53 VGPRs at 4 waves per SIMD, between the
+      // sums and the stores 51: not kept)
 #if PR_HOT_DIAG == 7
       {  // ladder 7: 64 extra dependent VALU instructions per unit (is VALU on the critical path?)
         uint32_t d = (uint32_t)lane;
