@@ -57,7 +57,7 @@ sys.path.insert(0, os.path.join(ROOT, "pagerank-using-apache-spark_amd"))
 METRIC = "PageRank GTEPS/iter + % HBM roofline, R-MAT scale-26 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); 6.29 TB/s measured copy
 # bumped whenever the SpMV pass changes, so a stale rocprof traffic figure is never reported
-LAYOUT_VERSION = "r6-split-c64-c20c24codes-grpparts-densecold-v14"
+LAYOUT_VERSION = "r6-split-c64-c20c24codes-grpparts-densecold256-v15"
 
 
 def log(msg: str) -> None:
